@@ -1,0 +1,228 @@
+"""Benchmark: YOLOv7 (COCO-80) 640x640 inference, bs=32 per GPU, on MI355X.
+
+One step = one batch through the whole hot path, device resident:
+  Model.forward (static plan of HIP kernels, one HIP graph replay)
+  -> fused decode + filter (ycx_decode_filter) -> sort + per-class NMS (ycx_sort_nms)
+  -> (N > 1) one RCCL all_gather of the padded detections over xGMI.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+For N > 1 launch with torch.distributed.run (one process per GPU); images are
+sharded by rank (weak scaling: 32 images per GPU per step).
+
+Prints ONE JSON line (rank 0) with images/s for the whole job, p50 step
+latency, the dominant kernel's roofline, and the CPU-oracle baseline.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "yolo-continuous_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+ANCHORS = [[12, 16, 19, 36, 40, 28], [36, 75, 76, 55, 72, 146], [142, 110, 192, 243, 459, 401]]
+MASK = [[6, 7, 8], [3, 4, 5], [0, 1, 2]]
+METRIC = "images/sec (whole node) + p50 end-to-end latency, 640×640 bs=32, 1/2/4/8 MI355X"
+PEAK = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
+    ap.add_argument("--size", type=int, default=640)
+    ap.add_argument("--net", default="yolov7")
+    ap.add_argument("--nc", type=int, default=80)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--conf", type=float, default=0.3)
+    ap.add_argument("--iou", type=float, default=0.3)
+    ap.add_argument("--max-det", type=int, default=300)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample (0: skip)")
+    ap.add_argument("--roofline-steps", type=int, default=3)
+    return ap.parse_args()
+
+
+def roofline(det, steps, precision):
+    """Per-op HIP events around every op of the plan (recorded on the plan's
+    stream by ycx_run_ops) for `steps` extra forwards; returns the dominant
+    conv kernel's achieved TFLOP/s and a per-kernel table."""
+    eng = det.engine
+    n = eng.n_ops
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+    for e in evs:  # materialise the underlying hipEvent_t
+        e.record()
+    per = {}
+    for _ in range(steps):
+        eng.run_static(events=evs)
+        torch.cuda.synchronize()
+        for i, info in enumerate(eng.op_info):
+            ms = evs[i].elapsed_time(evs[i + 1])
+            d = per.setdefault(info['name'], dict(ms=0.0, launches=0, flops=0))
+            d['ms'] += ms
+            d['launches'] += 1
+            d['flops'] += info.get('flops', 0)
+    for d in per.values():
+        d['ms'] /= steps
+        d['launches'] //= steps
+        d['flops'] //= steps
+    convs = {k: v for k, v in per.items() if v['flops'] > 0 and k != 'stem'}
+    dom = max(convs, key=lambda k: convs[k]['ms'])
+    dd = convs[dom]
+    avg_ms = dd['ms'] / dd['launches']
+    flops_per_launch = dd['flops'] / dd['launches']
+    achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+    all_conv_ms = sum(v['ms'] for v in per.values() if v['flops'] > 0)
+    all_conv_tf = sum(v['flops'] for v in per.values()) / (all_conv_ms * 1e-3) / 1e12
+    fwd_ms = sum(v['ms'] for v in per.values())
+    return dict(kernel=dom, avg_launch_ms=avg_ms, flops_per_launch=flops_per_launch, achieved=achieved,
+                all_conv_tflops=all_conv_tf, all_conv_ms=all_conv_ms, forward_kernel_ms=fwd_ms,
+                per_kernel={k: dict(ms=round(v['ms'], 4), launches=v['launches'],
+                                    tflops=(round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1) if v['flops'] else None))
+                            for k, v in sorted(per.items(), key=lambda kv: -kv[1]['ms'])})
+
+
+def cpu_baseline(args, sd, model_cfg, budget_s):
+    """The oracle (CPU fp32 restatement of the reference path: forward + decode_box
+    + non_max_suppression) on a bounded sample of the same workload."""
+    import numpy as np
+    from oracle import ref_forward, ref_post
+    from ycx.utils.synth import synthetic_images
+    cores = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(cores)
+    fwd = ref_forward.build(model_cfg, ANCHORS, args.nc, sd)
+    anchors = np.asarray(ANCHORS).reshape(-1, 2)
+    n = 2
+    x = synthetic_images(n, 3, args.size, args.size, seed=1)
+
+    def one():
+        heads = fwd(x)
+        dec = torch.cat(ref_post.decode_box(heads, anchors, MASK, args.nc, (args.size, args.size)), 1)
+        ref_post.non_max_suppression(dec, args.nc, (args.size, args.size), np.array([args.size, args.size]), True,
+                                     args.conf, args.iou)
+    one()  # warm-up
+    times = []
+    t_start = time.perf_counter()
+    while not times or (time.perf_counter() - t_start < budget_s and len(times) < 5):
+        t0 = time.perf_counter()
+        one()
+        times.append(time.perf_counter() - t0)
+    per_batch = statistics.median(times)
+    return dict(value=round(n / per_batch, 4), unit="images/s", cores=cores, kind="port",
+                sample=f"oracle forward+decode+NMS, {n} images {args.size}x{args.size} per batch, "
+                       f"{len(times)} timed batches (median {per_batch:.2f} s) + 1 warm-up, fp32, "
+                       f"torch {torch.__version__} CPU, {cores} threads")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ycx.detect import Detector
+    from ycx.nets.yolo import Model
+    from ycx.utils.helper_io import cvt_cfg
+    from ycx.utils.synth import synthetic_images, synthetic_state_dict
+
+    cfg = cvt_cfg(args.net)
+    model = Model(cfg, ANCHORS, args.nc, precision=args.precision).eval()
+    sd = synthetic_state_dict(model, seed=0)
+    model.load_state_dict(sd)
+    model.to(dev)
+    shape = (args.batch, 3, args.size, args.size)
+    det = Detector(model, shape, dev, ANCHORS, MASK, conf_thres=args.conf, nms_thres=args.iou,
+                   max_det=args.max_det, use_graph=not args.no_graph)
+    # Synthetic images, this rank's shard of the global batch, resident in HBM.
+    det.x.copy_(synthetic_images(*shape, seed=1000 + rank).to(dev))
+    if world > 1:
+        g_dets = torch.empty((world * args.batch, args.max_det, 7), dtype=torch.float32, device=dev)
+        g_cnt = torch.empty((world * args.batch,), dtype=torch.int32, device=dev)
+
+    def step():
+        dets, keep, kc = det()
+        if world > 1:  # the single collective: all-gather of padded detections (+ counts)
+            dist.all_gather_into_tensor(g_dets, dets)
+            dist.all_gather_into_tensor(g_cnt, kc)
+        return kc
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evs[0].record()
+    for i in range(args.steps):
+        kc = step()
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    lat = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    images = world * args.batch * args.steps
+    value = images / elapsed
+
+    rl = roofline(det, args.roofline_steps, args.precision) if rank == 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(args, sd, cfg, args.cpu_seconds)
+    if rank == 0:
+        peak = PEAK[args.precision]
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "p50_ms": round(statistics.median(lat), 4), "p90_ms": round(sorted(lat)[int(0.9 * (len(lat) - 1))], 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic U[0,1) images, seeded synthetic weights (no checkpoint exists)",
+            "config": {"workload": f"{args.net} COCO-{args.nc} {args.size}x{args.size}, {args.batch} images per GPU "
+                                   f"per step: forward + decode + NMS (+ all-gather)",
+                       "global_batch": world * args.batch, "per_gpu_batch": args.batch, "image_size": args.size,
+                       "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
+                       "conf_thres": args.conf, "iou_thres": args.iou, "max_det": args.max_det},
+            "mfma_fraction_whole_step": round(model.engine_for(shape, dev).flops_per_image * value /
+                                              (world * peak * 1e12), 4),
+            "roofline": {"bound": "mfma", "kernel": rl['kernel'], "achieved": round(rl['achieved'], 2), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(rl['achieved'] / peak, 4), "traffic": None,
+                         "avg_launch_ms": round(rl['avg_launch_ms'], 5),
+                         "flops_per_launch": int(rl['flops_per_launch']),
+                         "all_conv_tflops": round(rl['all_conv_tflops'], 2),
+                         "forward_kernel_ms": round(rl['forward_kernel_ms'], 4)},
+            "cpu_baseline": cpu,
+            "detections_last_step": int(kc.sum().item()),
+        }
+        print(json.dumps(out), flush=True)
+        if os.environ.get("YCX_BENCH_KERNELS"):
+            with open(os.environ["YCX_BENCH_KERNELS"], "w") as f:
+                json.dump(rl['per_kernel'], f, indent=1)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

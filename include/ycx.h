@@ -1,0 +1,201 @@
+/*
+ * ycx.h — C ABI of libycx_hip.so, the MI355X (gfx950) YOLO inference hot path.
+ *
+ * Every entry point is `extern "C"`, takes plain pointers/sizes, returns an
+ * int32 status (0 = OK) and launches asynchronously on the caller's HIP
+ * stream (passed as `void*`, i.e. a hipStream_t). The library never allocates
+ * device memory on the hot path: activations, packed weights, workspaces and
+ * outputs are owned by the caller (PyTorch's caching allocator in the Python
+ * host package).
+ *
+ * Reference interfaces each entry point replaces (xin-pu/yolo-continuous):
+ *   ycx_conv2d          Conv.forward = act(bn(conv2d(x)))      nets/common.py:97-109
+ *                       RepConv.forward (re-parameterised)      nets/common.py:477-495
+ *                       Detect head 1x1 convs (bias, no act)    nets/detect.py:27-38
+ *                       IDetect conv + ImplicitA/M (folded)     nets/idetect.py:26-31
+ *   ycx_stem_conv       first Conv on the fp32 NCHW image       nets/common.py:105-106 (Cin=3)
+ *   ycx_maxpool         MP / SP / SPPCSPC max-pools             nets/common.py:25-40, 257
+ *   ycx_copy_channels   nn.Upsample(None, 2, 'nearest')         cfg/net/yolov7.yaml:71,85
+ *                       Concat (only when a slice cannot alias)  nets/common.py:54-60
+ *   ycx_decode          decode_box (one head level)             detect.py:29-87
+ *   ycx_filter_decoded  non_max_suppression lines 98-121        detect.py:98-121
+ *   ycx_decode_filter   decode_box + the same filter, fused     detect.py:29-121
+ *   ycx_sort_nms        per-class torchvision.ops.nms loop      detect.py:124-137
+ *   ycx_run_ops         Model.forward layer loop                nets/yolo.py:143-153
+ */
+#ifndef YCX_H_
+#define YCX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YCX_ABI_VERSION 1
+
+typedef int32_t ycx_status;
+enum {
+  YCX_OK = 0,
+  YCX_ERR_BAD_ARG = 1,      /* null pointer, negative size, inconsistent shape  */
+  YCX_ERR_UNSUPPORTED = 2,  /* shape/dtype the kernels do not implement          */
+  YCX_ERR_LAUNCH = 3,       /* hipGetLastError() after a launch was not success   */
+  YCX_ERR_CAPACITY = 4      /* workspace / output capacity too small              */
+};
+
+enum { YCX_DT_BF16 = 0, YCX_DT_F32 = 1 };
+enum { YCX_ACT_NONE = 0, YCX_ACT_SILU = 1, YCX_ACT_LEAKY = 2 };
+enum {
+  YCX_OUT_NHWC = 0,       /* activation dtype, [N][Ho][Wo][out_c_stride] at out_c_off         */
+  YCX_OUT_NCHW_F32 = 1,   /* fp32 [N][out_c_stride][Ho][Wo] at out_c_off (Detect raw logits)   */
+  YCX_OUT_NHWC_UP2 = 2    /* activation dtype, each pixel written to its 2x2 block of a
+                             [N][2Ho][2Wo][out_c_stride] buffer (conv fused with nearest x2)   */
+};
+
+/* Convolution: NHWC activations, weights packed [cout_pad][kh][kw][cin] in the
+ * activation dtype, fp32 bias[cout_pad] (BN folded in). groups = 1. */
+typedef struct ycx_conv_desc {
+  int32_t n, h, w, cin, in_c_off, in_c_stride;
+  int32_t ho, wo, cout, cout_pad, out_c_off, out_c_stride;
+  int32_t kh, kw, stride, pad;
+  int32_t act;              /* YCX_ACT_*                                           */
+  float leaky_slope;        /* for YCX_ACT_LEAKY (0.1 in yolov7-tiny.yaml)          */
+  int32_t dtype;            /* YCX_DT_*: activations & weights                     */
+  int32_t out_layout;       /* YCX_OUT_*                                            */
+  int32_t res_c_off, res_c_stride; /* residual (same dtype/shape as the output)   */
+  int32_t tile;             /* 0 = auto, else a tile id (see ycx_conv_tile_name)    */
+} ycx_conv_desc;
+
+/* Max-pool, NHWC, pad value -inf (torch.nn.MaxPool2d semantics, floor mode). */
+typedef struct ycx_pool_desc {
+  int32_t n, h, w, c, in_c_off, in_c_stride;
+  int32_t ho, wo, out_c_off, out_c_stride;
+  int32_t k, stride, pad;
+  int32_t dtype;
+} ycx_pool_desc;
+
+/* Channel-slice copy with optional nearest x2 upsample (scale = 1 or 2).
+ * out_layout YCX_OUT_NHWC keeps the dtype; YCX_OUT_NCHW_F32 writes fp32
+ * [N][out_c_stride][Ho][Wo] (a model output that is not a Detect head). */
+typedef struct ycx_copy_desc {
+  int32_t n, h, w, c, in_c_off, in_c_stride;
+  int32_t out_c_off, out_c_stride;
+  int32_t scale;
+  int32_t dtype;
+  int32_t out_layout;
+} ycx_copy_desc;
+
+/* Decode of one head level (detect.py:29-87 semantics). head is fp32 NCHW
+ * [n][na*no][h][w]; out is fp32 [n][rows_total][no], written at row_off.
+ * anchors_scaled[2a], [2a+1] = anchor_w/stride_w, anchor_h/stride_h computed in
+ * double and rounded to fp32 exactly as detect.py:43-44 does. */
+typedef struct ycx_decode_desc {
+  int32_t n, h, w, na, no;
+  int32_t rows_total, row_off;
+  float anchors_scaled[16];
+} ycx_decode_desc;
+
+/* One NMS candidate (32 bytes): normalised xyxy box, objectness, best class
+ * confidence, best class id, row index into the concatenated [rows_total]. */
+typedef struct ycx_cand {
+  float x1, y1, x2, y2;
+  float obj, cls_conf;
+  int32_t cls, row;
+} ycx_cand;
+
+/* Filter of a decoded [n][rows][no] tensor (detect.py:98-121): xywh -> xyxy in
+ * place, class max (first index on ties), score = obj*cls_conf >= conf_thres. */
+typedef struct ycx_filter_desc {
+  int32_t n, rows, no, nc;
+  float conf_thres;         /* compared in fp32, as torch does for a float32 tensor */
+  int32_t write_xyxy;       /* 1: mutate pred[..., :4] to xyxy like detect.py:103  */
+} ycx_filter_desc;
+
+/* Fused decode + filter straight from the three fp32 NCHW head tensors. */
+typedef struct ycx_decode_filter_desc {
+  int32_t n, nl, na, no, nc;
+  int32_t h[4], w[4];       /* per level, in head order (P5, P4, P3 for Detect)    */
+  int32_t row_off[4];       /* first row of each level in the concatenated rows    */
+  int32_t rows_total;
+  float anchors_scaled[4][16];
+  float conf_thres;
+} ycx_decode_filter_desc;
+
+/* Per-image, per-class greedy NMS with torchvision.ops.nms semantics. */
+typedef struct ycx_nms_desc {
+  int32_t n, rows_total, nc;
+  int32_t max_det;          /* output rows per image (padded); counts are not capped */
+  double iou_thres;         /* compared as (double)iou > iou_thres, like torchvision */
+} ycx_nms_desc;
+
+/* A pre-built op for ycx_run_ops (the static execution plan of Model.forward). */
+enum { YCX_OP_CONV = 1, YCX_OP_STEM = 2, YCX_OP_POOL = 3, YCX_OP_COPY = 4 };
+typedef struct ycx_op {
+  int32_t kind;
+  int32_t pad_;
+  union {
+    ycx_conv_desc conv;
+    ycx_pool_desc pool;
+    ycx_copy_desc copy;
+  } d;
+  const void* in;           /* x                                                    */
+  const void* weight;       /* packed weights (conv/stem)                           */
+  const float* bias;        /* bias (conv/stem)                                     */
+  void* out;                /* y                                                    */
+  const void* residual;     /* optional residual (conv)                             */
+} ycx_op;
+
+int ycx_abi_version(void);
+/* sizeof() of the ABI structs, so FFI mirrors can verify their layout:
+ * 0 conv_desc, 1 pool_desc, 2 copy_desc, 3 decode_desc, 4 cand, 5 filter_desc,
+ * 6 decode_filter_desc, 7 nms_desc, 8 op. Returns 0 for an unknown id. */
+size_t ycx_struct_size(int32_t which);
+const char* ycx_strerror(ycx_status s);
+const char* ycx_conv_tile_name(int32_t tile);
+int32_t ycx_conv_pick_tile(const ycx_conv_desc* d);
+
+ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const void* w,
+                      const float* bias, void* y, const void* residual, void* stream);
+/* Stem conv: fp32 NCHW input (the model input, cin <= 4), weights fp32
+ * [kh][kw][cin][cout_pad], output NHWC in d->dtype. in_c_* describe the NCHW
+ * channel count (in_c_stride = channels of the input tensor). */
+ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, const float* w,
+                         const float* bias, void* y, void* stream);
+ycx_status ycx_maxpool(const ycx_pool_desc* d, const void* x, void* y, void* stream);
+ycx_status ycx_copy_channels(const ycx_copy_desc* d, const void* x, void* y, void* stream);
+
+ycx_status ycx_decode(const ycx_decode_desc* d, const float* head, float* out, void* stream);
+/* Candidate outputs of both filters:
+ *   cand        [n][rows] ycx_cand, written only at the rows that pass (dense by row)
+ *   cand_rows   [n][rows] int32, the passing row indices, compacted (any order)
+ *   cand_counts [n] int32, number of passing rows; MUST be zeroed before the call
+ *               (the filters append with wave-aggregated atomics). */
+ycx_status ycx_filter_decoded(const ycx_filter_desc* d, float* pred, ycx_cand* cand,
+                              int32_t* cand_rows, int32_t* cand_counts, void* stream);
+ycx_status ycx_decode_filter(const ycx_decode_filter_desc* d, const float* const* heads,
+                             ycx_cand* cand, int32_t* cand_rows, int32_t* cand_counts, void* stream);
+size_t ycx_nms_workspace_size(const ycx_nms_desc* d);
+/* Sorts each image's candidates by (class asc, score desc, row asc) — the order
+ * of detect.py:124-137 with a stable torchvision sort — and runs greedy NMS per
+ * class. Outputs: dets [n][max_det][7] = x1,y1,x2,y2,obj,cls_conf,cls (fp32),
+ * keep_rows [n][max_det] (row index, -1 padded), keep_counts [n] (not capped
+ * by max_det; rows beyond max_det are dropped from dets/keep_rows). */
+ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, const int32_t* cand_rows,
+                        const int32_t* cand_counts, void* workspace, size_t workspace_bytes,
+                        float* dets, int32_t* keep_rows, int32_t* keep_counts, void* stream);
+
+/* Run a static op list in order on one stream. If `events` is non-null it must
+ * hold n_ops+1 hipEvent_t; event i is recorded before op i and event n_ops
+ * after the last (per-op kernel timing for the roofline report). */
+ycx_status ycx_run_ops(const ycx_op* ops, int32_t n_ops, void* stream, void* const* events);
+
+/* Capture ycx_run_ops into a HIP graph and instantiate it (graph_exec out). */
+ycx_status ycx_graph_capture(const ycx_op* ops, int32_t n_ops, void* stream, void** graph_exec);
+ycx_status ycx_graph_launch(void* graph_exec, void* stream);
+ycx_status ycx_graph_destroy(void* graph_exec);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YCX_H_ */

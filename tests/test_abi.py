@@ -1,0 +1,67 @@
+"""The C-ABI library loads and exports every symbol include/ycx.h declares
+(no compute calls: runs without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "ycx.h")
+
+
+def header_symbols():
+    src = open(HDR).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(ycx_[a-z0-9_]+)\s*\(', src)))
+
+
+def test_header_declares_the_boundary():
+    syms = header_symbols()
+    for s in ('ycx_conv2d', 'ycx_stem_conv', 'ycx_maxpool', 'ycx_copy_channels', 'ycx_decode', 'ycx_filter_decoded',
+              'ycx_decode_filter', 'ycx_sort_nms', 'ycx_run_ops', 'ycx_strerror', 'ycx_abi_version'):
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol():
+    from ycx import _lib
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    for s in header_symbols():
+        assert hasattr(raw, s), f"{s} declared in ycx.h but not exported"
+        assert s in _lib.SYMBOLS, f"{s} not bound in ycx/_lib.py"
+
+
+def test_abi_metadata_without_gpu():
+    from ycx import _lib
+    assert _lib.lib.ycx_abi_version() == 1
+    for i, st in enumerate(_lib._STRUCTS):
+        assert _lib.lib.ycx_struct_size(i) == ctypes.sizeof(st)
+    assert _lib.lib.ycx_struct_size(99) == 0
+    assert b"bad argument" in _lib.lib.ycx_strerror(1)
+    assert _lib.lib.ycx_conv_tile_name(1) == b"bf16_co128_px128_k64"
+    # argument validation happens before any device call
+    assert _lib.lib.ycx_conv2d(None, None, None, None, None, None, None) == _lib.YCX_ERR_BAD_ARG
+    assert _lib.lib.ycx_sort_nms(None, None, None, None, None, 0, None, None, None, None) == _lib.YCX_ERR_BAD_ARG
+
+
+def test_tile_picker():
+    from ycx import _lib
+    d = _lib.ConvDesc()
+    d.n, d.ho, d.wo, d.cin, d.cout_pad, d.dtype = 32, 160, 160, 64, 64, _lib.DT_BF16
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 2
+    d.cin = 32
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 6
+    d.cout_pad = 32
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 5
+    d.cin, d.cout_pad, d.ho, d.wo = 512, 512, 20, 20
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) in (1, 4)
+    d.dtype = _lib.DT_F32
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 8
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    import subprocess
+    import sys
+    env = dict(os.environ, YCX_LIB=str(tmp_path / "nope.so"))
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "yolo-continuous_amd")
+    r = subprocess.run([sys.executable, "-c", "import ycx._lib"], cwd=pkg, env=env, capture_output=True, text=True)
+    assert r.returncode != 0 and "no CPU fallback" in r.stderr

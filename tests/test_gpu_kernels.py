@@ -1,0 +1,181 @@
+"""Kernel-level numerics through the C ABI vs a plain PyTorch fp32 (CPU, float64
+accumulate) reference of the same op on the same (bf16-rounded) operands."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+L = pytest.importorskip("ycx._lib")
+
+
+def _ref_conv(x_nchw, w, b, s, p, act, slope=0.1):
+    y = F.conv2d(x_nchw.double(), w.double(), b.double(), s, p)
+    if act == L.ACT_SILU:
+        y = F.silu(y)
+    elif act == L.ACT_LEAKY:
+        y = F.leaky_relu(y, slope)
+    return y
+
+
+def _run_conv(device, n, h, w, cin, cout, k, s, act, tile, dtype, in_extra=0, out_extra=0, residual=False,
+              layout=L.OUT_NHWC, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    tdt = torch.bfloat16 if dtype == L.DT_BF16 else torch.float32
+    p = k // 2
+    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    x = torch.randn(n, h, w, cin + in_extra, generator=g).to(tdt)           # NHWC, slice at in_extra
+    wt = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to(tdt)
+    b = torch.randn(cout, generator=g) * 0.1
+    cpad = -(-cout // 64) * 64 if dtype == L.DT_F32 else (32 if cout <= 32 else 64 if cout <= 64 else -(-cout // 128) * 128)
+    wp = torch.zeros(cpad, k, k, cin, dtype=tdt)
+    wp[:cout] = wt.permute(0, 2, 3, 1)
+    bp = torch.zeros(cpad)
+    bp[:cout] = b
+    up = 2 if layout == L.OUT_NHWC_UP2 else 1
+    if layout == L.OUT_NCHW_F32:
+        y = torch.zeros(n, cout, ho, wo, dtype=torch.float32)
+    else:
+        y = torch.zeros(n, ho * up, wo * up, cout + out_extra, dtype=tdt)
+    r = torch.randn(n, ho, wo, cout, generator=g).to(tdt) if residual else None
+    d = L.ConvDesc()
+    d.n, d.h, d.w, d.cin, d.in_c_off, d.in_c_stride = n, h, w, cin, in_extra, cin + in_extra
+    d.ho, d.wo, d.cout, d.cout_pad = ho, wo, cout, cpad
+    d.out_c_off, d.out_c_stride = (0, cout) if layout == L.OUT_NCHW_F32 else (out_extra, cout + out_extra)
+    d.kh = d.kw = k
+    d.stride, d.pad, d.act, d.leaky_slope = s, p, act, 0.1
+    d.dtype, d.out_layout = dtype, layout
+    d.res_c_off, d.res_c_stride = 0, cout
+    d.tile = tile
+    xd, wd, bd, yd = x.to(device), wp.contiguous().to(device), bp.to(device), y.to(device)
+    rd = r.to(device) if r is not None else None
+    st = L.check(L.lib.ycx_conv2d(ctypes.byref(d), xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), yd.data_ptr(),
+                                  rd.data_ptr() if rd is not None else None, L.stream_handle(device)))
+    torch.cuda.synchronize()
+    ref = _ref_conv(x[..., in_extra:].permute(0, 3, 1, 2).float(), wt.float(), b, s, p, act)
+    if residual:
+        ref = ref + r.permute(0, 3, 1, 2).double()
+    got = yd.cpu()
+    if layout == L.OUT_NCHW_F32:
+        got = got.double()
+    elif layout == L.OUT_NHWC_UP2:
+        got = got[..., out_extra:].permute(0, 3, 1, 2).double()
+        ref = ref.repeat_interleave(2, 2).repeat_interleave(2, 3)
+    else:
+        got = got[..., out_extra:].permute(0, 3, 1, 2).double()
+        assert torch.all(yd.cpu()[..., :out_extra] == 0), "wrote outside the output channel slice"
+    return got, ref
+
+
+TILES_BF16 = [(1, 128, 64), (2, 64, 64), (3, 64, 64), (4, 128, 64), (5, 32, 32), (6, 64, 32), (7, 128, 32)]
+
+
+@pytest.mark.parametrize('tile,cout,cin', TILES_BF16)
+@pytest.mark.parametrize('k,s', [(3, 1), (1, 1), (3, 2)])
+def test_conv_bf16_tiles(device, tile, cout, cin, k, s):
+    got, ref = _run_conv(device, 2, 13, 11, cin, cout, k, s, L.ACT_SILU, tile, L.DT_BF16, in_extra=8, out_extra=16)
+    # bf16 output rounding (2^-8 relative) on top of exact products of bf16 inputs
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize('cin,cout,k,s', [(32, 64, 3, 1), (64, 128, 3, 2), (128, 255, 1, 1), (64, 32, 1, 1)])
+def test_conv_f32(device, cin, cout, k, s):
+    layout = L.OUT_NCHW_F32 if cout == 255 else L.OUT_NHWC
+    got, ref = _run_conv(device, 2, 9, 10, cin, cout, k, s, L.ACT_LEAKY, 0, L.DT_F32, layout=layout)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_conv_heads_nchw_bf16(device):
+    got, ref = _run_conv(device, 3, 20, 20, 256, 255, 1, 1, L.ACT_NONE, 0, L.DT_BF16, layout=L.OUT_NCHW_F32)
+    torch.testing.assert_close(got, ref, rtol=1e-3, atol=1e-3)  # fp32 output: only accumulation order differs
+
+
+def test_conv_residual_and_up2(device):
+    got, ref = _run_conv(device, 2, 8, 8, 64, 64, 3, 1, L.ACT_SILU, 0, L.DT_BF16, residual=True)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=2e-2)
+    got, ref = _run_conv(device, 2, 5, 7, 128, 128, 1, 1, L.ACT_SILU, 0, L.DT_BF16, layout=L.OUT_NHWC_UP2,
+                         out_extra=8)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+    got, ref = _run_conv(device, 2, 5, 7, 64, 64, 1, 1, L.ACT_NONE, 0, L.DT_F32, layout=L.OUT_NHWC_UP2, residual=False)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_conv_rejects_bad_shapes(device):
+    d = L.ConvDesc()
+    d.n, d.h, d.w, d.cin, d.in_c_stride, d.ho, d.wo, d.cout, d.cout_pad = 1, 8, 8, 24, 24, 8, 8, 64, 64
+    d.out_c_stride, d.kh, d.kw, d.stride, d.pad, d.dtype = 64, 3, 3, 1, 1, L.DT_BF16
+    t = torch.zeros(1 << 16, device=device)
+    s = L.lib.ycx_conv2d(ctypes.byref(d), t.data_ptr(), t.data_ptr(), t.data_ptr(), t.data_ptr(), None,
+                         L.stream_handle(device))
+    assert s == L.YCX_ERR_UNSUPPORTED  # cin 24 is not a multiple of the 32-wide K step
+    d.cin, d.in_c_stride, d.ho = 32, 32, 7
+    assert L.lib.ycx_conv2d(ctypes.byref(d), t.data_ptr(), t.data_ptr(), t.data_ptr(), t.data_ptr(), None,
+                            L.stream_handle(device)) == L.YCX_ERR_BAD_ARG
+    assert L.lib.ycx_conv2d(None, None, None, None, None, None, None) == L.YCX_ERR_BAD_ARG
+
+
+@pytest.mark.parametrize('dtype', [L.DT_BF16, L.DT_F32])
+@pytest.mark.parametrize('k,s,p', [(2, 2, 0), (5, 1, 2), (9, 1, 4), (13, 1, 6), (3, 2, 1)])
+def test_maxpool(device, dtype, k, s, p):
+    tdt = torch.bfloat16 if dtype == L.DT_BF16 else torch.float32
+    n, h, w, c = 2, 11, 13, 32
+    x = torch.randn(n, h, w, c + 8).to(tdt)
+    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    y = torch.zeros(n, ho, wo, c + 16, dtype=tdt)
+    d = L.PoolDesc()
+    d.n, d.h, d.w, d.c, d.in_c_off, d.in_c_stride = n, h, w, c, 8, c + 8
+    d.ho, d.wo, d.out_c_off, d.out_c_stride, d.k, d.stride, d.pad, d.dtype = ho, wo, 16, c + 16, k, s, p, dtype
+    xd, yd = x.to(device), y.to(device)
+    L.check(L.lib.ycx_maxpool(ctypes.byref(d), xd.data_ptr(), yd.data_ptr(), L.stream_handle(device)))
+    ref = F.max_pool2d(x[..., 8:].permute(0, 3, 1, 2).float(), k, s, p).permute(0, 2, 3, 1)
+    assert torch.equal(yd.cpu()[..., 16:].float(), ref)  # max is exact
+
+
+@pytest.mark.parametrize('dtype', [L.DT_BF16, L.DT_F32])
+@pytest.mark.parametrize('scale,nchw', [(1, False), (2, False), (1, True)])
+def test_copy_upsample(device, dtype, scale, nchw):
+    tdt = torch.bfloat16 if dtype == L.DT_BF16 else torch.float32
+    n, h, w, c = 2, 5, 6, 16
+    x = torch.randn(n, h, w, c + 8).to(tdt)
+    d = L.CopyDesc()
+    d.n, d.h, d.w, d.c, d.in_c_off, d.in_c_stride, d.scale, d.dtype = n, h, w, c, 8, c + 8, scale, dtype
+    ref = F.interpolate(x[..., 8:].permute(0, 3, 1, 2).float(), scale_factor=scale, mode='nearest')
+    if nchw:
+        y = torch.zeros(n, c, h, w, dtype=torch.float32)
+        d.out_c_off, d.out_c_stride, d.out_layout = 0, c, L.OUT_NCHW_F32
+    else:
+        y = torch.zeros(n, h * scale, w * scale, c + 24, dtype=tdt)
+        d.out_c_off, d.out_c_stride, d.out_layout = 24, c + 24, L.OUT_NHWC
+    xd, yd = x.to(device), y.to(device)
+    L.check(L.lib.ycx_copy_channels(ctypes.byref(d), xd.data_ptr(), yd.data_ptr(), L.stream_handle(device)))
+    got = yd.cpu().float() if nchw else yd.cpu()[..., 24:].permute(0, 3, 1, 2).float()
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize('cin,k,s', [(3, 3, 1), (3, 3, 2), (1, 3, 1)])
+@pytest.mark.parametrize('dtype', [L.DT_BF16, L.DT_F32])
+def test_stem(device, cin, k, s, dtype):
+    n, h, w, cout = 2, 17, 19, 32
+    x = torch.rand(n, cin, h, w)
+    wt = torch.randn(cout, cin, k, k) * 0.3
+    b = torch.randn(cout) * 0.1
+    p = k // 2
+    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    tdt = torch.bfloat16 if dtype == L.DT_BF16 else torch.float32
+    y = torch.zeros(n, ho, wo, cout, dtype=tdt)
+    d = L.ConvDesc()
+    d.n, d.h, d.w, d.cin, d.in_c_off, d.in_c_stride = n, h, w, cin, 0, cin
+    d.ho, d.wo, d.cout, d.cout_pad, d.out_c_off, d.out_c_stride = ho, wo, cout, cout, 0, cout
+    d.kh = d.kw = k
+    d.stride, d.pad, d.act, d.leaky_slope, d.dtype, d.out_layout = s, p, L.ACT_SILU, 0.1, dtype, L.OUT_NHWC
+    wd = wt.permute(2, 3, 1, 0).contiguous().to(device)
+    xd, bd, yd = x.to(device), b.to(device), y.to(device)
+    L.check(L.lib.ycx_stem_conv(ctypes.byref(d), xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), yd.data_ptr(),
+                                L.stream_handle(device)))
+    ref = _ref_conv(x, wt, b, s, p, L.ACT_SILU)
+    got = yd.cpu().permute(0, 3, 1, 2).double()
+    tol = 1e-2 if dtype == L.DT_BF16 else 1e-5
+    torch.testing.assert_close(got, ref, rtol=tol, atol=tol)

@@ -1,0 +1,83 @@
+"""Pin the oracle: CPU restatement vs golden vectors made by the reference itself.
+
+The fixtures (tests/golden/make_golden.py) come from importing
+xin-pu/yolo-continuous in the build container; these tests prove the oracle
+reproduces them, so the GPU parity tests can use the oracle as the checker at
+any size.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import ANCHORS, MASK, arr_hash, g1_case, g3_heads, make_model, sd_hash
+from oracle import ref_forward, ref_post
+from ycx.utils.helper_io import cvt_cfg
+from ycx.utils.synth import synthetic_images
+
+G1_NAMES = ['conv_k3s1_cin32', 'conv_k3s2_cin32', 'conv_k1_cin64', 'conv_leaky', 'stem_s2_leaky', 'pools',
+            'upsample_concat', 'upsample_shared', 'sppcspc', 'repconv', 'csp_blocks', 'detect', 'idetect']
+
+
+def _close(a, b):
+    # Same ATen ops in the same order on the same CPU: identical up to oneDNN
+    # thread/ISA-dependent reassociation (observed bit-exact in the build container).
+    np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6 * max(1.0, float(np.abs(b).max())))
+
+
+@pytest.mark.parametrize('name', G1_NAMES)
+def test_oracle_g1(manifest, g1, name):
+    m, sd, x, e = g1_case(manifest, name)
+    assert len(sd) == e['n_keys']
+    assert sd_hash(sd) == e['sd_hash'], "synthetic weights / state_dict schema drifted from the fixture"
+    fwd = ref_forward.build(e['cfg'], ANCHORS, e['nc'], sd)
+    out = fwd(x)
+    outs = out if isinstance(out, list) else [out]
+    assert len(outs) == e['n_out']
+    for j, o in enumerate(outs):
+        gold = g1[f'{name}/{j}']
+        if name == 'idetect':  # oracle returns NCHW maps; the fixture is the reference's (bs,na,ny,nx,no) view
+            bs, _, ny, nx = o.shape
+            o = o.view(bs, 3, -1, ny, nx).permute(0, 1, 3, 4, 2)
+        _close(o.numpy(), gold)
+
+
+@pytest.mark.parametrize('name', ['yolov7_160', 'tiny_640'])
+def test_oracle_g2(manifest, g2, name):
+    e = manifest['g2'][name]
+    m, sd = make_model(e['net'], e['nc'], e['w_seed'])
+    assert len(sd) == e['n_keys'] and sd_hash(sd) == e['sd_hash']
+    x = synthetic_images(*e['shape'], seed=e['img_seed'])
+    outs = ref_forward.build(cvt_cfg(e['net']), ANCHORS, e['nc'], sd)(x)
+    for j, o in enumerate(outs):
+        _close(o.numpy(), g2[f'{name}/{j}'])
+
+
+@pytest.mark.parametrize('name', ['coco80_bs4', 'nc1_bs2', 'nc3_dense'])
+def test_oracle_g3(manifest, g3, name):
+    e = manifest['g3'][name]
+    heads = g3_heads(e)
+    assert arr_hash([h.numpy() for h in heads]) == e['heads_hash']
+    anchors = np.asarray(ANCHORS).reshape(-1, 2)
+    dec = torch.cat(ref_post.decode_box(heads, anchors, MASK, e['nc'], (e['size'], e['size'])), 1)
+    assert arr_hash([dec.numpy()]) == e['decoded_hash'], "decode_box restatement is not bit-exact"
+    for b in range(e['bs']):
+        rows = g3[f'{name}/pass_rows/{b}']
+        np.testing.assert_array_equal(dec[b, rows].numpy(), g3[f'{name}/pass_vals/{b}'])
+    keep, _ = ref_post.nms_keep_rows(dec.clone(), e['nc'], e['conf'], e['iou'])
+    final = ref_post.non_max_suppression(dec.clone(), e['nc'], (e['size'], e['size']),
+                                         np.array(e['image_shape']), True, e['conf'], e['iou'])
+    for b in range(e['bs']):
+        np.testing.assert_array_equal(keep[b].numpy(), g3[f'{name}/keep_rows/{b}'])
+        np.testing.assert_array_equal(final[b], g3[f'{name}/final/{b}'])
+
+
+def test_nms_restatement_semantics():
+    """torchvision.ops.nms contract: score-descending keep, stable ties, '>' threshold."""
+    boxes = torch.tensor([[0, 0, 10, 10], [0, 0, 10, 10], [1, 1, 11, 11], [50, 50, 60, 60]], dtype=torch.float32)
+    scores = torch.tensor([0.9, 0.9, 0.8, 0.95])
+    assert ref_post.nms(boxes, scores, 0.5).tolist() == [3, 0]
+    # IoU of boxes 0 and 2 is 81/119 = 0.68: equal-to-threshold is kept, strictly above is suppressed
+    iou02 = float(np.float32(81) / (np.float32(100) + np.float32(100) - np.float32(81)))
+    assert ref_post.nms(boxes[[0, 2]], scores[[0, 2]], iou02).tolist() == [0, 1]
+    assert ref_post.nms(boxes[[0, 2]], scores[[0, 2]], iou02 - 1e-6).tolist() == [0]
+    assert ref_post.nms(boxes[:0], scores[:0], 0.5).numel() == 0

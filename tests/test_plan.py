@@ -1,0 +1,86 @@
+"""Host-side (CPU) checks of the builder, the lowering passes and the weight folding."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import ANCHORS, make_model
+from ycx.engine import Plan, fold_bn, fold_repconv
+from ycx.nets.common import RepConv
+from ycx.nets.yolo import Model, parse_model
+from ycx.utils.helper_io import cvt_cfg
+
+
+def test_parse_model_matches_reference_bookkeeping(manifest):
+    m = Model(cvt_cfg('yolov7'), ANCHORS, 80)
+    assert len(m.model) == 106 and len(m.save) == 62          # SURVEY.md §3.2 [measured]
+    assert len(m.state_dict()) == 558
+    assert sum(p.numel() for p in m.parameters()) == 37620125  # SURVEY.md §6 [measured]
+    t = Model(cvt_cfg('yolov7-tiny'), ANCHORS, 1)
+    assert len(t.model) == 78 and len(t.save) == 51
+    assert sum(p.numel() for p in t.parameters()) == 6014038
+    assert manifest['g2']['yolov7_160']['n_keys'] == 558 and manifest['g2']['tiny_640']['n_keys'] == 336
+
+
+def test_safe_parser_rejects_out_of_scope_and_unknown():
+    d = {'depth_multiple': 1.0, 'width_multiple': 1.0, 'backbone': [[-1, 1, 'GhostConv', [32, 3, 1]]], 'head': []}
+    with pytest.raises(NotImplementedError, match='out of scope'):
+        parse_model(d, [3], ANCHORS, 1)
+    d['backbone'][0][2] = '__import__("os")'
+    with pytest.raises(ValueError, match='unknown module'):
+        parse_model(d, [3], ANCHORS, 1)
+
+
+@pytest.mark.parametrize('net,nc,gflop', [('yolov7', 80, 104.5110784), ('yolov7-tiny', 1, 13.021184)])
+def test_plan_flops_and_passes(net, nc, gflop):
+    m = Model(cvt_cfg(net), ANCHORS, nc)
+    plan = Plan(m, (1, 3, 640, 640))
+    assert abs(plan.conv_flops / 1e9 - gflop) < 1e-6  # SURVEY.md §8(d) folded FLOP/img
+    c = plan.counts()
+    assert c.get('up', 0) == 0, "both nearest-x2 upsamples should be fused into their producer convs"
+    assert c.get('copy', 0) == 0, "every concat input should alias its slice"
+    assert len(plan.out_vals) == 3 and [v.h for v in plan.out_vals] == [20, 40, 80]
+
+
+def test_plan_yolov7_layout():
+    plan = Plan(Model(cvt_cfg('yolov7'), ANCHORS, 80), (2, 3, 640, 640))
+    c = plan.counts()
+    assert c['stem'] == 1 and c['conv'] + c['stem'] == 92  # 95 convs minus the 3 folded RepConv 1x1 branches
+    assert c['pool'] == 8  # 5 MP (k2s2) + the SPPCSPC 5/9/13 set as a 3-deep k5 cascade
+    assert all(nd.p['k'] in (2, 5) for nd in plan.graph.nodes if nd.kind == 'pool')
+
+
+def test_fold_bn_and_repconv_exact():
+    torch.manual_seed(0)
+    for c1, c2, s in ((16, 32, 1), (32, 32, 1), (16, 16, 2)):
+        m = RepConv(c1, c2, 3, s).eval().double()
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.uniform_(-0.5, 0.5)
+                mod.running_var.uniform_(0.5, 1.5)
+                mod.weight.data.uniform_(0.5, 1.5)
+                mod.bias.data.uniform_(-0.5, 0.5)
+        x = torch.randn(2, c1, 9, 9, dtype=torch.float64)
+        bn = lambda b, v: F.batch_norm(v, b.running_mean, b.running_var, b.weight, b.bias, False, 0.0, b.eps)
+        ref = bn(m.rbr_dense[1], F.conv2d(x, m.rbr_dense[0].weight, None, s, 1)) + \
+            bn(m.rbr_1x1[1], F.conv2d(x, m.rbr_1x1[0].weight, None, s, 0))
+        if m.rbr_identity is not None:
+            ref = ref + bn(m.rbr_identity, x)
+        w, b = fold_repconv(m)
+        torch.testing.assert_close(F.conv2d(x, w, b, s, 1), ref, rtol=1e-12, atol=1e-12)
+    conv = torch.nn.Conv2d(8, 16, 3, 1, 1, bias=False).double()
+    bnm = torch.nn.BatchNorm2d(16).double().eval()
+    bnm.running_var.uniform_(0.5, 2.0)
+    bnm.running_mean.uniform_(-1, 1)
+    x = torch.randn(1, 8, 7, 7, dtype=torch.float64)
+    w, b = fold_bn(conv.weight, bnm)
+    torch.testing.assert_close(F.conv2d(x, w, b, 1, 1), bnm(conv(x)), rtol=1e-12, atol=1e-12)
+
+
+def test_state_dict_roundtrip_and_invalidation():
+    m, sd = make_model('yolov7-tiny', 1, 0)
+    m._engines['sentinel'] = type('E', (), {'close': lambda self: None})()
+    m.load_state_dict(sd)
+    assert m._engines == {}, "load_state_dict must drop compiled plans (packed weights)"
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, sd[k])

@@ -1,0 +1,594 @@
+// Implicit-GEMM convolution for gfx950 (CDNA4), NHWC activations.
+//
+// Replaces Conv.forward = act(bn(conv2d(x))) (nets/common.py:97-109), the
+// re-parameterised RepConv (nets/common.py:477-495) and the Detect / IDetect
+// 1x1 head convs (nets/detect.py:27-38, nets/idetect.py:26-31). BN, RepConv
+// branches and ImplicitA/M are folded into (weight, bias) by the host prepack.
+//
+// GEMM view: D[co][px] = sum_k Wt[co][k] * X[px][k], k = (ky*kw + kx)*cin + ci.
+//   A operand = packed weights  [cout_pad][kh*kw*cin]  (K contiguous)
+//   B operand = NHWC activations, im2col-on-the-fly     (K contiguous per tap)
+// Both operands are K-major, which is exactly the lane layout of
+// v_mfma_f32_16x16x32_bf16 (lane l holds 8 consecutive k of row l&15), so
+// every LDS fragment read is one ds_read_b128.
+//
+// bf16 path: 256 threads = 4 waves, tile BM(co) x BN(px) x BK, register-staged
+// double-buffered LDS with an XOR swizzle (conflict-free ds_read_b128, checked
+// by brute force), one barrier per K step, XCD-aware block remap, fp32
+// accumulate, epilogue = bias + act (+ residual), staged through LDS as fp32 and
+// written with 16-byte coalesced stores into a channel slice of the consumer's
+// concat buffer (Concat is never materialised).
+//
+// f32 path ("parity mode"): same structure on v_mfma_f32_16x16x4_f32 (exact
+// fp32 FMA chain), used to prove the 1e-3 relative bound vs the fp32 CPU
+// reference.
+#include "ycx_internal.h"
+
+namespace {
+
+struct ConvArgs {
+  const void* x;
+  const void* w;
+  const float* bias;
+  void* y;
+  const void* res;
+  int N, H, W, Cin, in_coff, in_cs;
+  int Ho, Wo, Cout, Cout_pad, out_coff, out_cs;
+  int KH, KW, S, P;
+  int act;
+  float slope;
+  int out_layout;
+  int res_coff, res_cs;
+  int M, HoWo, Ktot, nsteps, n_ct, nwg;
+};
+
+template <int BK>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (BK == 64) return (row >> 1) & 7;
+  else return (-(row >> 2)) & 3;
+}
+
+// Writes 8 consecutive output channels of pixel p (fp32 values v) to the
+// output, NHWC or NHWC-upsampled-x2, adding the residual first if present.
+template <typename T>
+__device__ __forceinline__ void store8(const ConvArgs& a, int p, int co, float v[8]) {
+  if (a.res) {
+    const T* r = reinterpret_cast<const T*>(a.res) + (size_t)p * a.res_cs + a.res_coff + co;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 rv = *reinterpret_cast<const bf16x8*>(r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
+    } else {
+      f32x4 r0 = *reinterpret_cast<const f32x4*>(r), r1 = *reinterpret_cast<const f32x4*>(r + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] += r0[j]; v[4 + j] += r1[j]; }
+    }
+  }
+  T* base = reinterpret_cast<T*>(a.y);
+  auto put = [&](size_t pix) {
+    T* o = base + pix * a.out_cs + a.out_coff + co;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 ov;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ov[j] = (__bf16)v[j];
+      *reinterpret_cast<bf16x8*>(o) = ov;
+    } else {
+      *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  };
+  if (a.out_layout == YCX_OUT_NHWC_UP2) {
+    int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    size_t W2 = 2 * (size_t)a.Wo;
+    size_t b0 = ((size_t)n * 2 * a.Ho + 2 * oy) * W2 + 2 * ox;
+    put(b0); put(b0 + 1); put(b0 + W2); put(b0 + W2 + 1);
+  } else {
+    put((size_t)p);
+  }
+}
+
+// -------------------------------------------------------------------------
+// bf16 MFMA kernel
+// -------------------------------------------------------------------------
+template <int BM, int BN, int BK, int WM, int WN>
+__global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int TM = BM / WM, TN = BN / WN;  // per-wave tile (co x px)
+  constexpr int FM = TM / 16, FN = TN / 16;  // 16x16 MFMA tiles per wave
+  constexpr int CPR = BK / 8;                // 16-byte chunks per LDS row
+  constexpr int RPP = 256 / CPR;             // rows covered by one pass of 256 threads
+  constexpr int ACH = (BM + RPP - 1) / RPP;  // A chunks per thread
+  constexpr int BCH = (BN + RPP - 1) / RPP;  // B chunks per thread
+  constexpr int A_EL = BM * BK, B_EL = BN * BK;
+  constexpr int STAGE_BYTES = 2 * (A_EL + B_EL) * 2;
+  constexpr int CP = BM + 4;                 // fp32 C staging pitch (floats)
+  constexpr int C_BYTES = BN * CP * 4;
+  constexpr int LDS_BYTES = STAGE_BYTES > C_BYTES ? STAGE_BYTES : C_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  __bf16* As = reinterpret_cast<__bf16*>(smem);  // [2][BM*BK]
+  __bf16* Bs = As + 2 * A_EL;                    // [2][BN*BK]
+
+  const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
+  const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
+  const int ct = L % a.n_ct, pt = L / a.n_ct;
+  const int co0 = ct * BM, px0 = pt * BN;
+  const int ch = tid % CPR;
+
+  // Per-thread B rows: output pixel -> top-left input position.
+  int b_iy0[BCH], b_ix0[BCH], b_nh[BCH];
+  bool b_ok[BCH];
+#pragma unroll
+  for (int i = 0; i < BCH; ++i) {
+    int row = tid / CPR + i * RPP;
+    int p = px0 + row;
+    bool ok = (row < BN) && (p < a.M);
+    int pp = ok ? p : 0;
+    int n = pp / a.HoWo, rem = pp - n * a.HoWo;
+    int oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    b_iy0[i] = oy * a.S - a.P;
+    b_ix0[i] = ox * a.S - a.P;
+    b_nh[i] = n * a.H;
+    b_ok[i] = ok;
+  }
+
+  bf16x8 ra[ACH], rb[BCH];
+  const bf16x8 zero8 = {};
+  auto gload = [&](int s, int ky, int kx, int cblk) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      int row = tid / CPR + i * RPP;
+      if (row < BM)
+        ra[i] = *reinterpret_cast<const bf16x8*>(Wt + (size_t)(co0 + row) * a.Ktot + s * BK + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      int iy = b_iy0[i] + ky, ix = b_ix0[i] + kx;
+      bool ok = b_ok[i] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      rb[i] = ok ? *reinterpret_cast<const bf16x8*>(
+                       X + ((size_t)(b_nh[i] + iy) * a.W + ix) * a.in_cs + a.in_coff + cblk + ch * 8)
+                 : zero8;
+    }
+  };
+  auto lstore = [&](int buf) {
+    __bf16* A = As + buf * A_EL;
+    __bf16* B = Bs + buf * B_EL;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      int row = tid / CPR + i * RPP;
+      if (row < BM) *reinterpret_cast<bf16x8*>(A + row * BK + ((ch ^ swz<BK>(row)) << 3)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      int row = tid / CPR + i * RPP;
+      if (row < BN) *reinterpret_cast<bf16x8*>(B + row * BK + ((ch ^ swz<BK>(row)) << 3)) = rb[i];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const __bf16* A = As + buf * A_EL;
+    const __bf16* B = Bs + buf * B_EL;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int c = kk * 4 + (lane >> 4);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        int row = wm * TM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(A + row * BK + ((c ^ swz<BK>(row)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        int row = wn * TN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(B + row * BK + ((c ^ swz<BK>(row)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // K loop: step s <-> (tap (ky,kx), channel block cblk).
+  int ky = 0, kx = 0, cblk = 0;
+  gload(0, 0, 0, 0);
+  lstore(0);
+  __syncthreads();
+  for (int s = 0; s < a.nsteps; ++s) {
+    const bool more = s + 1 < a.nsteps;
+    if (more) {
+      cblk += BK;
+      if (cblk == a.Cin) {
+        cblk = 0;
+        if (++kx == a.KW) { kx = 0; ++ky; }
+      }
+      gload(s + 1, ky, kx, cblk);
+    }
+    compute(s & 1);
+    if (more) lstore((s + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  if (a.out_layout == YCX_OUT_NCHW_F32) {
+    float* Y = reinterpret_cast<float*>(a.y);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        int p = px0 + wn * TN + j * 16 + (lane & 15);
+        if (p >= a.M) continue;
+        int n = p / a.HoWo, rem = p - n * a.HoWo;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int co = co0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          if (co < a.Cout) {
+            float v = ycx_act<true>(acc[i][j][r] + a.bias[co], a.act, a.slope);
+            Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] = v;
+          }
+        }
+      }
+    return;
+  }
+  float* Cs = reinterpret_cast<float*>(smem);  // [BN][CP]
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    int col = wm * TM + i * 16 + (lane >> 4) * 4;
+    f32x4 bv = *reinterpret_cast<const f32x4*>(a.bias + co0 + col);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      int row = wn * TN + j * 16 + (lane & 15);
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = ycx_act<true>(acc[i][j][r] + bv[r], a.act, a.slope);
+      *reinterpret_cast<f32x4*>(Cs + row * CP + col) = v;
+    }
+  }
+  __syncthreads();
+  constexpr int CCH = BM / 8;
+  for (int idx = tid; idx < BN * CCH; idx += 256) {
+    int row = idx / CCH, c8 = idx - row * CCH;
+    int p = px0 + row, co = co0 + c8 * 8;
+    if (p >= a.M || co >= a.Cout) continue;
+    f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * CP + c8 * 8);
+    f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * CP + c8 * 8 + 4);
+    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    store8<__bf16>(a, p, co, v);
+  }
+}
+
+// -------------------------------------------------------------------------
+// fp32 parity kernel: 64x64 tile, BK=16, v_mfma_f32_16x16x4_f32.
+// -------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) conv_f32_kernel(ConvArgs a) {
+  constexpr int BM = 64, BN = 64, BK = 16, TM = 32, TN = 32, FM = 2, FN = 2;
+  __shared__ __attribute__((aligned(16))) float As[2][BM * BK];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * BK];
+  const float* __restrict__ X = reinterpret_cast<const float*>(a.x);
+  const float* __restrict__ Wt = reinterpret_cast<const float*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
+  const int ct = L % a.n_ct, pt = L / a.n_ct;
+  const int co0 = ct * BM, px0 = pt * BN;
+  const int ch = tid & 3, row = tid >> 2;  // one 16-B chunk of A and of B per thread
+  auto sw = [](int r) { return (r >> 1) & 3; };
+
+  int p = px0 + row;
+  bool pok = p < a.M;
+  int pp = pok ? p : 0;
+  int n = pp / a.HoWo, rem = pp - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+  int iy0 = oy * a.S - a.P, ix0 = ox * a.S - a.P, nh = n * a.H;
+
+  f32x4 ra, rb;
+  auto gload = [&](int s, int ky, int kx, int cblk) {
+    ra = *reinterpret_cast<const f32x4*>(Wt + (size_t)(co0 + row) * a.Ktot + s * BK + ch * 4);
+    int iy = iy0 + ky, ix = ix0 + kx;
+    bool ok = pok && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+    rb = ok ? *reinterpret_cast<const f32x4*>(X + ((size_t)(nh + iy) * a.W + ix) * a.in_cs + a.in_coff +
+                                              cblk + ch * 4)
+            : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto lstore = [&](int buf) {
+    *reinterpret_cast<f32x4*>(&As[buf][row * BK + ((ch ^ sw(row)) << 2)]) = ra;
+    *reinterpret_cast<f32x4*>(&Bs[buf][row * BK + ((ch ^ sw(row)) << 2)]) = rb;
+  };
+  f32x4 acc[FM][FN];
+  for (int i = 0; i < FM; ++i)
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int ky = 0, kx = 0, cblk = 0;
+  gload(0, 0, 0, 0);
+  lstore(0);
+  __syncthreads();
+  for (int s = 0; s < a.nsteps; ++s) {
+    const bool more = s + 1 < a.nsteps;
+    if (more) {
+      cblk += BK;
+      if (cblk == a.Cin) {
+        cblk = 0;
+        if (++kx == a.KW) { kx = 0; ++ky; }
+      }
+      gload(s + 1, ky, kx, cblk);
+    }
+    const int buf = s & 1;
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {  // k = kk*4 + (lane>>4): chunk kk, element lane>>4
+      float af[FM], bf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        int r = wm * TM + i * 16 + (lane & 15);
+        af[i] = As[buf][r * BK + ((kk ^ sw(r)) << 2) + (lane >> 4)];
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        int r = wn * TN + j * 16 + (lane & 15);
+        bf[j] = Bs[buf][r * BK + ((kk ^ sw(r)) << 2) + (lane >> 4)];
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) lstore((s + 1) & 1);
+    __syncthreads();
+  }
+
+  // Epilogue: lane holds 4 consecutive output channels of one pixel per tile.
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      int pe = px0 + wn * TN + j * 16 + (lane & 15);
+      int cb = co0 + wm * TM + i * 16 + (lane >> 4) * 4;
+      if (pe >= a.M) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = ycx_act<false>(acc[i][j][r] + a.bias[cb + r], a.act, a.slope);
+      if (a.out_layout == YCX_OUT_NCHW_F32) {
+        int n2 = pe / a.HoWo, rem2 = pe - n2 * a.HoWo;
+        float* Y = reinterpret_cast<float*>(a.y);
+        for (int r = 0; r < 4; ++r)
+          if (cb + r < a.Cout) Y[((size_t)n2 * a.out_cs + a.out_coff + cb + r) * a.HoWo + rem2] = v[r];
+        continue;
+      }
+      if (cb >= a.Cout) continue;
+      if (a.res) {
+        f32x4 rv = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.res) +
+                                                    (size_t)pe * a.res_cs + a.res_coff + cb);
+        for (int r = 0; r < 4; ++r) v[r] += rv[r];
+      }
+      float* Y = reinterpret_cast<float*>(a.y);
+      f32x4 ov = {v[0], v[1], v[2], v[3]};
+      if (a.out_layout == YCX_OUT_NHWC_UP2) {
+        int n2 = pe / a.HoWo, rem2 = pe - n2 * a.HoWo, oy2 = rem2 / a.Wo, ox2 = rem2 - oy2 * a.Wo;
+        size_t W2 = 2 * (size_t)a.Wo;
+        size_t b0 = ((size_t)n2 * 2 * a.Ho + 2 * oy2) * W2 + 2 * ox2;
+        size_t q[4] = {b0, b0 + 1, b0 + W2, b0 + W2 + 1};
+        for (int t = 0; t < 4; ++t) *reinterpret_cast<f32x4*>(Y + q[t] * a.out_cs + a.out_coff + cb) = ov;
+      } else {
+        *reinterpret_cast<f32x4*>(Y + (size_t)pe * a.out_cs + a.out_coff + cb) = ov;
+      }
+    }
+}
+
+// -------------------------------------------------------------------------
+// Stem: first conv on the fp32 NCHW model input (cin <= 4). VALU direct conv,
+// one thread per output pixel, folded weights broadcast from LDS.
+// -------------------------------------------------------------------------
+template <int KH, int KW, int CIN, typename OutT>
+__global__ void __launch_bounds__(256) stem_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float ws[];  // [KH*KW*CIN][Cout_pad] + bias
+  constexpr int NT = KH * KW * CIN;
+  const float* Wt = reinterpret_cast<const float*>(a.w);
+  const int wn = NT * a.Cout_pad;
+  for (int i = threadIdx.x; i < wn; i += blockDim.x) ws[i] = Wt[i];
+  for (int i = threadIdx.x; i < a.Cout_pad; i += blockDim.x) ws[wn + i] = a.bias[i];
+  __syncthreads();
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.M) return;
+  const int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+  const float* X = reinterpret_cast<const float*>(a.x);
+  float patch[NT];
+#pragma unroll
+  for (int ky = 0; ky < KH; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < KW; ++kx) {
+      int iy = oy * a.S - a.P + ky, ix = ox * a.S - a.P + kx;
+      bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci)
+        patch[(ky * KW + kx) * CIN + ci] =
+            ok ? X[(((size_t)n * a.in_cs + a.in_coff + ci) * a.H + iy) * a.W + ix] : 0.0f;
+    }
+  for (int c0 = 0; c0 < a.Cout; c0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      f32x4 w0 = *reinterpret_cast<const f32x4*>(ws + t * a.Cout_pad + c0);
+      f32x4 w1 = *reinterpret_cast<const f32x4*>(ws + t * a.Cout_pad + c0 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = fmaf(patch[t], w0[j], v[j]);
+        v[4 + j] = fmaf(patch[t], w1[j], v[4 + j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = ycx_act<sizeof(OutT) == 2>(v[j] + ws[wn + c0 + j], a.act, a.slope);
+    store8<OutT>(a, p, c0, v);
+  }
+}
+
+ConvArgs make_args(const ycx_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                   const void* res) {
+  ConvArgs a;
+  a.x = x; a.w = w; a.bias = bias; a.y = y; a.res = res;
+  a.N = d->n; a.H = d->h; a.W = d->w; a.Cin = d->cin; a.in_coff = d->in_c_off; a.in_cs = d->in_c_stride;
+  a.Ho = d->ho; a.Wo = d->wo; a.Cout = d->cout; a.Cout_pad = d->cout_pad;
+  a.out_coff = d->out_c_off; a.out_cs = d->out_c_stride;
+  a.KH = d->kh; a.KW = d->kw; a.S = d->stride; a.P = d->pad;
+  a.act = d->act; a.slope = d->leaky_slope; a.out_layout = d->out_layout;
+  a.res_coff = d->res_c_off; a.res_cs = d->res_c_stride;
+  a.M = d->n * d->ho * d->wo; a.HoWo = d->ho * d->wo; a.Ktot = d->kh * d->kw * d->cin;
+  a.nsteps = 0; a.n_ct = 0; a.nwg = 0;
+  return a;
+}
+
+struct TileInfo {
+  int bm, bn, bk;
+  const char* name;
+};
+// Tile ids (ycx_conv_desc.tile): 1..N. Keep in sync with launch_bf16 below.
+const TileInfo kTiles[] = {
+    {0, 0, 0, "auto"},
+    {128, 128, 64, "bf16_co128_px128_k64"},
+    {64, 256, 64, "bf16_co64_px256_k64"},
+    {64, 128, 64, "bf16_co64_px128_k64"},
+    {128, 64, 64, "bf16_co128_px64_k64"},
+    {32, 256, 32, "bf16_co32_px256_k32"},
+    {64, 256, 32, "bf16_co64_px256_k32"},
+    {128, 128, 32, "bf16_co128_px128_k32"},
+    {64, 64, 16, "f32_co64_px64_k16"},
+};
+constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
+
+template <int BM, int BN, int BK, int WM, int WN>
+ycx_status launch_bf16(ConvArgs a, hipStream_t st) {
+  a.nsteps = a.KH * a.KW * (a.Cin / BK);
+  a.n_ct = a.Cout_pad / BM;
+  int n_pt = (a.M + BN - 1) / BN;
+  a.nwg = a.n_ct * n_pt;
+  hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, BK, WM, WN>), dim3(a.nwg), dim3(256), 0, st, a);
+  return ycx_launch_status();
+}
+
+}  // namespace
+
+extern "C" const char* ycx_conv_tile_name(int32_t tile) {
+  if (tile < 0 || tile >= kNumTiles) return "invalid";
+  return kTiles[tile].name;
+}
+
+// Tile heuristic: pick the largest tile that still gives >= ~2 waves of blocks
+// on 256 CUs, with BK = 32 only where cin is not a multiple of 64.
+extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {
+  if (!d) return 0;
+  if (d->dtype == YCX_DT_F32) return 8;
+  const long long M = (long long)d->n * d->ho * d->wo;
+  const bool k64 = (d->cin % 64) == 0;
+  if (d->cout_pad % 64 != 0) return 5;  // cout 32: co32 x px256, BK 32 (cin % 32 == 0)
+  if (!k64) {
+    if (d->cout_pad % 128 == 0 && d->cout_pad >= 128) return 7;
+    if (d->cout_pad % 64 == 0) return 6;
+    return 5;
+  }
+  if (d->cout_pad % 128 == 0) {
+    long long blocks = (d->cout_pad / 128) * ((M + 127) / 128);
+    if (blocks >= 512) return 1;
+    return 4;  // co128 x px64: twice the blocks for small-M (deep) layers
+  }
+  if (d->cout_pad % 64 == 0) {
+    long long blocks = (d->cout_pad / 64) * ((M + 255) / 256);
+    if (blocks >= 512) return 2;
+    return 3;
+  }
+  return 0;
+}
+
+extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const void* w, const float* bias,
+                                 void* y, const void* residual, void* stream) {
+  YCX_CHECK_ARG(d && x && w && bias && y);
+  YCX_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->cin > 0 && d->cout > 0 && d->ho > 0 && d->wo > 0);
+  YCX_CHECK_ARG(d->kh > 0 && d->kw > 0 && d->stride > 0 && d->pad >= 0);
+  YCX_CHECK_ARG(d->cout_pad >= d->cout && d->in_c_off >= 0 && d->in_c_off + d->cin <= d->in_c_stride);
+  YCX_CHECK_ARG(d->ho == (d->h + 2 * d->pad - d->kh) / d->stride + 1);
+  YCX_CHECK_ARG(d->wo == (d->w + 2 * d->pad - d->kw) / d->stride + 1);
+  YCX_CHECK_ARG(d->out_c_off >= 0);
+  YCX_CHECK_ARG(d->out_layout == YCX_OUT_NCHW_F32 || d->out_c_off + d->cout <= d->out_c_stride);
+  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32);
+  YCX_CHECK_SUPPORTED(d->out_layout >= YCX_OUT_NHWC && d->out_layout <= YCX_OUT_NHWC_UP2);
+  YCX_CHECK_SUPPORTED(d->act >= YCX_ACT_NONE && d->act <= YCX_ACT_LEAKY);
+  YCX_CHECK_SUPPORTED(!residual || d->out_layout == YCX_OUT_NHWC);
+  const int vec = d->dtype == YCX_DT_BF16 ? 8 : 4;
+  YCX_CHECK_SUPPORTED(d->in_c_off % vec == 0 && d->in_c_stride % vec == 0);
+  if (d->out_layout != YCX_OUT_NCHW_F32)
+    YCX_CHECK_SUPPORTED(d->cout % 8 == 0 && d->out_c_off % 8 == 0 && d->out_c_stride % 8 == 0);
+  if (residual) YCX_CHECK_SUPPORTED(d->res_c_off % 8 == 0 && d->res_c_stride % 8 == 0);
+  // The 32-bit index math inside the kernels.
+  YCX_CHECK_SUPPORTED((long long)d->n * d->ho * d->wo < (1LL << 31));
+  YCX_CHECK_SUPPORTED((long long)d->cout_pad * d->kh * d->kw * d->cin < (1LL << 31));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ConvArgs a = make_args(d, x, w, bias, y, residual);
+
+  int tile = d->tile ? d->tile : ycx_conv_pick_tile(d);
+  YCX_CHECK_SUPPORTED(tile > 0 && tile < kNumTiles);
+  const TileInfo& t = kTiles[tile];
+  YCX_CHECK_SUPPORTED(d->cin % t.bk == 0 && d->cout_pad % t.bm == 0);
+  if (d->dtype == YCX_DT_F32) {
+    YCX_CHECK_SUPPORTED(tile == 8);
+    a.nsteps = a.KH * a.KW * (a.Cin / 16);
+    a.n_ct = a.Cout_pad / 64;
+    a.nwg = a.n_ct * ((a.M + 63) / 64);
+    hipLaunchKernelGGL(conv_f32_kernel, dim3(a.nwg), dim3(256), 0, st, a);
+    return ycx_launch_status();
+  }
+  switch (tile) {
+    case 1: return launch_bf16<128, 128, 64, 2, 2>(a, st);
+    case 2: return launch_bf16<64, 256, 64, 1, 4>(a, st);
+    case 3: return launch_bf16<64, 128, 64, 2, 2>(a, st);
+    case 4: return launch_bf16<128, 64, 64, 2, 2>(a, st);
+    case 5: return launch_bf16<32, 256, 32, 1, 4>(a, st);
+    case 6: return launch_bf16<64, 256, 32, 1, 4>(a, st);
+    case 7: return launch_bf16<128, 128, 32, 2, 2>(a, st);
+    default: return YCX_ERR_UNSUPPORTED;
+  }
+}
+
+extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, const float* w, const float* bias,
+                                    void* y, void* stream) {
+  YCX_CHECK_ARG(d && x && w && bias && y);
+  YCX_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->cout > 0 && d->cout_pad >= d->cout);
+  YCX_CHECK_ARG(d->ho == (d->h + 2 * d->pad - d->kh) / d->stride + 1);
+  YCX_CHECK_ARG(d->wo == (d->w + 2 * d->pad - d->kw) / d->stride + 1);
+  YCX_CHECK_ARG(d->in_c_off >= 0 && d->in_c_off + d->cin <= d->in_c_stride);
+  YCX_CHECK_SUPPORTED(d->cout % 8 == 0 && d->cout_pad % 8 == 0 && d->out_c_off % 8 == 0 &&
+                      d->out_c_stride % 8 == 0 && d->out_c_off + d->cout <= d->out_c_stride);
+  YCX_CHECK_SUPPORTED(d->out_layout == YCX_OUT_NHWC || d->out_layout == YCX_OUT_NHWC_UP2);
+  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32);
+  YCX_CHECK_SUPPORTED((long long)d->n * d->ho * d->wo < (1LL << 31));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ConvArgs a = make_args(d, x, w, bias, y, nullptr);
+  const size_t lds = ((size_t)d->kh * d->kw * d->cin * d->cout_pad + d->cout_pad) * sizeof(float);
+  YCX_CHECK_SUPPORTED(lds <= 64 * 1024);
+  dim3 grid(ycx_cdiv(a.M, 256));
+  const bool bf = d->dtype == YCX_DT_BF16;
+#define YCX_STEM(KH_, KW_, CI_)                                                                  \
+  if (d->kh == KH_ && d->kw == KW_ && d->cin == CI_) {                                           \
+    if (bf)                                                                                      \
+      hipLaunchKernelGGL((stem_kernel<KH_, KW_, CI_, __bf16>), grid, dim3(256), lds, st, a);     \
+    else                                                                                         \
+      hipLaunchKernelGGL((stem_kernel<KH_, KW_, CI_, float>), grid, dim3(256), lds, st, a);      \
+    return ycx_launch_status();                                                                  \
+  }
+  YCX_STEM(3, 3, 3)
+  YCX_STEM(3, 3, 1)
+  YCX_STEM(3, 3, 4)
+  YCX_STEM(1, 1, 3)
+  YCX_STEM(5, 5, 3)
+  YCX_STEM(6, 6, 3)
+#undef YCX_STEM
+  return YCX_ERR_UNSUPPORTED;
+}

@@ -1,0 +1,273 @@
+"""Inference entry points (drop-in for the reference detect.py) on the HIP kernels.
+
+Reference API kept (same names, argument meaning, return types):
+  decode_box(inputs, anchors, anchors_mask, num_labels, image_size)      detect.py:29-87
+  non_max_suppression(prediction, num_classes, input_shape, image_shape,
+                      letterbox_image, conf_thres=0.5, nms_thres=0.4)    detect.py:90-144
+  yolo_correct_boxes(box_xy, box_wh, input_shape, image_shape, letterbox) detect.py:147-165
+  prepare_model(plan)                                                     detect.py:168-180
+  predict(cfg_file, image_path, conf_threshold=0.3, nms_threshold=0.3)   detect.py:208-265
+
+Device tensors in, device kernels doing the work: decode_box runs ycx_decode
+per level; non_max_suppression runs ycx_filter_decoded (which also mutates
+``prediction[..., :4]`` to xyxy in place, like detect.py:98-103) and
+ycx_sort_nms, then copies the kept rows to the host for the numpy
+``yolo_correct_boxes`` step, exactly where the reference leaves the device.
+
+``Detector`` is the fused fast path used by bench.py: forward -> fused
+decode+filter -> sort+NMS, all on device, static buffers, optional HIP graph.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+def _scaled_anchors(anchors, mask, image_size0, h, w):
+    """anchor / stride with stride = image_size[0] / grid (detect.py:38-44): float64
+    division, then rounded to fp32 like FloatTensor(scaled_anchors)."""
+    a = np.asarray(anchors).reshape(-1, 2)
+    sw, sh = image_size0 / w, image_size0 / h
+    return [np.float32(aw / sw) for aw, _ in a[mask]], [np.float32(ah / sh) for _, ah in a[mask]]
+
+
+def _require_device(t, what):
+    if not isinstance(t, torch.Tensor) or t.device.type != 'cuda':
+        raise RuntimeError(f"ycx: {what} must be a tensor on a ROCm device (there is no CPU path)")
+
+
+def decode_box(inputs, anchors, anchors_mask, num_labels, image_size=(640, 640)):
+    """list of fp32 NCHW heads [bs, na*(5+nc), H, W] -> list of [bs, na*H*W, 5+nc].
+    The per-level outputs are views of one [bs, sum(rows), 5+nc] tensor, so
+    ``torch.cat(outputs, 1)`` (detect.py:230) is a copy the caller may skip via
+    ``decode_box.last_concat``."""
+    no = num_labels + 5
+    bs = inputs[0].shape[0]
+    rows = [len(anchors_mask[i]) * p.shape[2] * p.shape[3] for i, p in enumerate(inputs)]
+    out = torch.empty((bs, sum(rows), no), dtype=torch.float32, device=inputs[0].device)
+    stream = L.stream_handle(out.device)
+    off, views = 0, []
+    for i, pred in enumerate(inputs):
+        _require_device(pred, "decode_box input")
+        pred = pred.float().contiguous()
+        na = len(anchors_mask[i])
+        if pred.shape[1] != na * no:
+            raise ValueError(f"ycx: head {i} has {pred.shape[1]} channels, expected {na}*{no}")
+        h, w = pred.shape[2], pred.shape[3]
+        aw, ah = _scaled_anchors(anchors, anchors_mask[i], image_size[0], h, w)
+        d = L.DecodeDesc()
+        d.n, d.h, d.w, d.na, d.no, d.rows_total, d.row_off = bs, h, w, na, no, sum(rows), off
+        for a in range(na):
+            d.anchors_scaled[2 * a], d.anchors_scaled[2 * a + 1] = aw[a], ah[a]
+        L.check(L.lib.ycx_decode(ctypes.byref(d), pred.data_ptr(), out.data_ptr(), stream), "ycx_decode")
+        views.append(out[:, off:off + rows[i]])
+        off += rows[i]
+    decode_box.last_concat = out
+    return views
+
+
+def _nms_buffers(n, rows, device):
+    cand = torch.empty((n, rows, 8), dtype=torch.float32, device=device)  # ycx_cand, 32 B
+    cand_rows = torch.empty((n, rows), dtype=torch.int32, device=device)
+    counts = torch.zeros((n,), dtype=torch.int32, device=device)
+    return cand, cand_rows, counts
+
+
+def device_nms(cand, cand_rows, counts, nc, iou_thres, max_det):
+    """ycx_sort_nms -> (dets [n, max_det, 7], keep_rows [n, max_det], keep_counts [n]) on device."""
+    n, rows = cand.shape[0], cand.shape[1]
+    d = L.NmsDesc()
+    d.n, d.rows_total, d.nc, d.max_det, d.iou_thres = n, rows, nc, max_det, float(iou_thres)
+    ws_bytes = int(L.lib.ycx_nms_workspace_size(ctypes.byref(d)))
+    ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=cand.device)
+    dets = torch.empty((n, max_det, 7), dtype=torch.float32, device=cand.device)
+    keep = torch.empty((n, max_det), dtype=torch.int32, device=cand.device)
+    kc = torch.empty((n,), dtype=torch.int32, device=cand.device)
+    L.check(L.lib.ycx_sort_nms(ctypes.byref(d), cand.data_ptr(), cand_rows.data_ptr(), counts.data_ptr(),
+                               ws.data_ptr(), ws_bytes, dets.data_ptr(), keep.data_ptr(), kc.data_ptr(),
+                               L.stream_handle(cand.device)), "ycx_sort_nms")
+    return dets, keep, kc
+
+
+def nms_device(prediction, num_classes, conf_thres=0.5, nms_thres=0.4, max_det=None, write_xyxy=True):
+    """Device part of non_max_suppression: returns (dets, keep_rows, keep_counts)."""
+    _require_device(prediction, "prediction")
+    if prediction.dtype != torch.float32 or not prediction.is_contiguous():
+        raise ValueError("ycx: prediction must be a contiguous fp32 tensor")
+    n, rows, no = prediction.shape
+    cand, cand_rows, counts = _nms_buffers(n, rows, prediction.device)
+    f = L.FilterDesc()
+    f.n, f.rows, f.no, f.nc, f.conf_thres, f.write_xyxy = n, rows, no, num_classes, float(conf_thres), int(write_xyxy)
+    L.check(L.lib.ycx_filter_decoded(ctypes.byref(f), prediction.data_ptr(), cand.data_ptr(), cand_rows.data_ptr(),
+                                     counts.data_ptr(), L.stream_handle(prediction.device)), "ycx_filter_decoded")
+    return device_nms(cand, cand_rows, counts, num_classes, nms_thres, max_det or rows)
+
+
+def non_max_suppression(prediction, num_classes, input_shape, image_shape, letterbox_image, conf_thres=0.5,
+                        nms_thres=0.4):
+    """detect.py:90-144 semantics: list (per image) of np.float32 [K, 7] rows
+    (y1, x1, y2, x2 in original-image pixels, obj, cls_conf, cls) or None."""
+    dets, _, kc = nms_device(prediction, num_classes, conf_thres, nms_thres)
+    counts = kc.cpu().numpy()
+    dets = dets.cpu().numpy()
+    output = [None] * prediction.shape[0]
+    for i in range(prediction.shape[0]):
+        k = int(counts[i])
+        if k == 0:
+            continue
+        o = dets[i, :k].copy()
+        box_xy, box_wh = (o[:, 0:2] + o[:, 2:4]) / 2, o[:, 2:4] - o[:, 0:2]
+        o[:, :4] = yolo_correct_boxes(box_xy, box_wh, input_shape, image_shape, letterbox_image)
+        output[i] = o
+    return output
+
+
+def yolo_correct_boxes(box_xy, box_wh, input_shape, image_shape, letterbox_image):
+    """Undo the letterbox (numpy, host): returns [y1, x1, y2, x2] in pixels (detect.py:147-165)."""
+    box_yx = box_xy[..., ::-1]
+    box_hw = box_wh[..., ::-1]
+    input_shape = np.array(input_shape)
+    image_shape = np.array(image_shape)
+    if letterbox_image:
+        new_shape = np.round(image_shape * np.min(input_shape / image_shape))
+        offset = (input_shape - new_shape) / 2. / input_shape
+        scale = input_shape / new_shape
+        box_yx = (box_yx - offset) * scale
+        box_hw *= scale
+    box_mins = box_yx - (box_hw / 2.)
+    box_maxes = box_yx + (box_hw / 2.)
+    boxes = np.concatenate([box_mins[..., 0:1], box_mins[..., 1:2], box_maxes[..., 0:1], box_maxes[..., 1:2]],
+                           axis=-1)
+    boxes *= np.concatenate([image_shape, image_shape], axis=-1)
+    return boxes
+
+
+class Detector:
+    """Fused device pipeline for a fixed batch shape: Model forward (static plan,
+    optionally one HIP graph) -> ycx_decode_filter -> ycx_sort_nms.
+
+    Outputs stay on device: dets [n, max_det, 7] (normalised xyxy, obj,
+    cls_conf, cls), keep_rows [n, max_det] (row into the concatenated
+    [sum na*H*W] candidates, -1 padded), keep_counts [n] (uncapped)."""
+
+    def __init__(self, model, shape, device, anchors, anchors_mask, image_size=None, conf_thres=0.3,
+                 nms_thres=0.3, max_det=300, use_graph=True):
+        self.model = model
+        self.engine = model.engine_for(shape, device)
+        self.device = torch.device(device)
+        n, _, H, W = shape
+        image_size = image_size or (H, W)
+        self.x, heads = self.engine.bind_static(torch.zeros(shape, dtype=torch.float32, device=device))
+        if not isinstance(heads, list):
+            raise ValueError("ycx: Detector needs a model whose last layer is a Detect head")
+        self.heads = heads
+        nc = model.num_classes
+        d = L.DecodeFilterDesc()
+        d.n, d.nl, d.na, d.no, d.nc = n, len(heads), len(anchors_mask[0]), nc + 5, nc
+        off = 0
+        for l, hd in enumerate(heads):
+            h, w = hd.shape[2], hd.shape[3]
+            d.h[l], d.w[l], d.row_off[l] = h, w, off
+            aw, ah = _scaled_anchors(anchors, anchors_mask[l], image_size[0], h, w)
+            for a in range(len(aw)):
+                d.anchors_scaled[l][2 * a], d.anchors_scaled[l][2 * a + 1] = aw[a], ah[a]
+            off += len(anchors_mask[l]) * h * w
+        d.rows_total, d.conf_thres = off, float(conf_thres)
+        self.rows = off
+        self.df_desc = d
+        self.heads_arr = (ctypes.c_void_p * 4)(*[h.data_ptr() for h in heads], *([None] * (4 - len(heads))))
+        self.cand, self.cand_rows, self.counts = _nms_buffers(n, off, device)
+        nd = L.NmsDesc()
+        nd.n, nd.rows_total, nd.nc, nd.max_det, nd.iou_thres = n, off, nc, max_det, float(nms_thres)
+        self.nms_desc = nd
+        self.ws_bytes = int(L.lib.ycx_nms_workspace_size(ctypes.byref(nd)))
+        self.ws = torch.empty((self.ws_bytes,), dtype=torch.uint8, device=device)
+        self.dets = torch.empty((n, max_det, 7), dtype=torch.float32, device=device)
+        self.keep = torch.empty((n, max_det), dtype=torch.int32, device=device)
+        self.kc = torch.empty((n,), dtype=torch.int32, device=device)
+        self.use_graph = use_graph
+        if use_graph:
+            self.engine.capture()
+
+    def post(self):
+        st = L.stream_handle(self.device)
+        self.counts.zero_()
+        L.check(L.lib.ycx_decode_filter(ctypes.byref(self.df_desc), self.heads_arr, self.cand.data_ptr(),
+                                        self.cand_rows.data_ptr(), self.counts.data_ptr(), st), "ycx_decode_filter")
+        L.check(L.lib.ycx_sort_nms(ctypes.byref(self.nms_desc), self.cand.data_ptr(), self.cand_rows.data_ptr(),
+                                   self.counts.data_ptr(), self.ws.data_ptr(), self.ws_bytes, self.dets.data_ptr(),
+                                   self.keep.data_ptr(), self.kc.data_ptr(), st), "ycx_sort_nms")
+        return self.dets, self.keep, self.kc
+
+    def __call__(self, images=None, events=None):
+        if images is not None:
+            self.x.copy_(images)
+        if self.use_graph and events is None:
+            self.engine.replay()
+        else:
+            self.engine.run_static(events)
+        return self.post()
+
+
+def prepare_model(plan, weights=None, device=None, precision='bf16'):
+    """detect.py:168-180: build the Model from the plan and load its weights.
+    ``weights`` overrides plan.save_path (a state_dict or a path, loaded with
+    weights_only=True); 'synthetic' loads the seeded recipe of ycx.utils.synth."""
+    from .nets.yolo import Model, WeightInitial
+    from .utils.helper_io import cvt_cfg
+    net = Model(cvt_cfg(plan.model_cfg), plan.anchors, plan.num_labels, image_chan=plan.image_chan,
+                weight_initial=WeightInitial.Random, precision=precision)
+    src = weights if weights is not None else plan.save_path
+    if isinstance(src, str) and src == 'synthetic':
+        from .utils.synth import synthetic_state_dict
+        sd = synthetic_state_dict(net, seed=0)
+    elif isinstance(src, dict):
+        sd = src
+    else:
+        sd = torch.load(src, map_location='cpu', weights_only=True)
+    net.load_state_dict(sd)
+    net = net.eval()
+    if device is not None:
+        net = net.to(device)
+    return net
+
+
+def predict(cfg_file, image_path=None, conf_threshold=0.3, nms_threshold=0.3, *, image=None, device=None,
+            weights=None, show=False):
+    """detect.py:208-265, headless by default. ``image`` may be an HWC uint8 BGR
+    array instead of a path. Returns the list of TargetBox-like dicts it prints."""
+    from .cfg.train_plan import TrainPlan
+    from .utils.helper_io import check_file
+    from .utils.helper_torch import select_device
+    from .utils.letterbox import letterbox, read_image
+    plan = TrainPlan(check_file(cfg_file))
+    dev = select_device(device if device is not None else plan.device)
+    target = (plan.image_size, plan.image_size)
+    anchors = np.asarray(plan.anchors).reshape(-1, 2)
+    original = image if image is not None else read_image(image_path)
+    data = letterbox(original, target)
+    data = np.expand_dims(np.transpose(data.astype(np.float32) / 255., (2, 0, 1)), 0)
+    net = prepare_model(plan, weights=weights, device=dev)
+    images = torch.from_numpy(data).to(dev)
+    with torch.no_grad():
+        pred = net(images)
+    outputs = decode_box(pred, anchors, plan.anchors_mask, plan.num_labels, image_size=target)
+    all_outputs = torch.cat(outputs, 1)
+    results = non_max_suppression(all_outputs, plan.num_labels, target, np.array(original.shape[0:2]), True,
+                                  conf_thres=conf_threshold, nms_thres=nms_threshold)
+    boxes = []
+    if results[0] is not None:
+        r = results[0]
+        for row in r:
+            y1, x1, y2, x2 = row[0], row[1], row[2], row[3]
+            box = [max(0, int(np.floor(x1))), max(0, int(np.floor(y1))),
+                   min(original.shape[1], int(np.floor(x2))), min(original.shape[0], int(np.floor(y2)))]
+            label = int(row[6])
+            boxes.append(dict(box=box, score=float(row[4] * row[5]), label=plan.labels[label]))
+            print(f"{plan.labels[label]}\t{row[4] * row[5]:.3f}\t{box}")
+    return boxes

@@ -1,0 +1,581 @@
+"""Static execution plan of ``Model.forward`` on the HIP kernels.
+
+Lowering (once per input shape / device / precision):
+
+1. Walk ``model.model`` exactly like the reference interpreter loop
+   (nets/yolo.py:143-153: ``m.f`` indexing into the per-layer outputs) and lower
+   each module into graph nodes — conv (BN folded, RepConv re-parameterised,
+   Bottleneck residual fused into the epilogue), stem conv (first conv on the
+   fp32 NCHW image), max-pool, upsample, concat, Detect/IDetect heads.
+2. Passes: nearest-x2 upsample fused into its producing conv's store
+   (YCX_OUT_NHWC_UP2); the SPPCSPC 5/9/13 pools run as a k5 cascade (exact for
+   max with -inf padding); every concat input that a kernel produces is written
+   straight into its channel slice of the concat buffer (Concat costs nothing;
+   a copy kernel runs only for inputs that cannot alias).
+3. Allocate one NHWC device buffer per remaining value (no reuse: a yolov7
+   bs=32 640x640 plan is ~10 GB of bf16 activations, small next to 288 GB HBM),
+   pack weights ([cout_pad][kh][kw][cin], bf16 or fp32) and build the ctypes
+   op array consumed by the native loop ``ycx_run_ops`` (or a HIP graph).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib as L
+from .nets.common import (SP, SPP, SPPCSPC, SPPF, MP, Bottleneck, BottleneckCSPA, BottleneckCSPB, BottleneckCSPC,
+                          Concat, Conv, RepConv)
+from .nets.detect import Detect, IDetect
+
+
+class Buf:
+    __slots__ = ('n', 'h', 'w', 'c', 'tensor')
+
+    def __init__(self, n, h, w, c):
+        self.n, self.h, self.w, self.c, self.tensor = n, h, w, c, None
+
+
+class Val:
+    """An activation: channels [coff, coff + c) of an NHWC buffer."""
+    __slots__ = ('n', 'h', 'w', 'c', 'buf', 'coff', 'producer', 'consumers', 'role')
+
+    def __init__(self, n, h, w, c, role='act'):
+        self.n, self.h, self.w, self.c = n, h, w, c
+        self.buf, self.coff, self.producer, self.consumers, self.role = None, 0, None, [], role
+
+
+class Node:
+    __slots__ = ('kind', 'inputs', 'out', 'p')
+
+    def __init__(self, kind, inputs, out, **p):
+        self.kind, self.inputs, self.out, self.p = kind, inputs, out, p
+
+
+def _pair(v):
+    return v if isinstance(v, (tuple, list)) else (v, v)
+
+
+def _square(v, what):
+    a, b = _pair(v)
+    if a != b:
+        raise NotImplementedError(f"ycx: non-square {what} {v}")
+    return int(a)
+
+
+def fold_bn(weight, bn):
+    """conv weight (+BN) -> float64 (W, b): W*gamma/std, beta - mean*gamma/std
+    (nets/common.py:14-17, 503-529)."""
+    w = weight.detach().to('cpu', torch.float64)
+    if bn is None:
+        return w, torch.zeros(w.shape[0], dtype=torch.float64)
+    std = (bn.running_var.detach().to('cpu', torch.float64) + bn.eps).sqrt()
+    t = bn.weight.detach().to('cpu', torch.float64) / std
+    b = bn.bias.detach().to('cpu', torch.float64) - bn.running_mean.detach().to('cpu', torch.float64) * t
+    return w * t.reshape(-1, 1, 1, 1), b
+
+
+def fold_repconv(m: RepConv):
+    """RepConv -> one 3x3 conv (get_equivalent_kernel_bias, nets/common.py:488-529)."""
+    if hasattr(m, 'rbr_reparam'):
+        c = m.rbr_reparam
+        b = c.bias.detach().to('cpu', torch.float64) if c.bias is not None else torch.zeros(c.out_channels,
+                                                                                               dtype=torch.float64)
+        return c.weight.detach().to('cpu', torch.float64), b
+    k3, b3 = fold_bn(m.rbr_dense[0].weight, m.rbr_dense[1])
+    k1, b1 = fold_bn(m.rbr_1x1[0].weight, m.rbr_1x1[1])
+    k = k3 + torch.nn.functional.pad(k1, [1, 1, 1, 1])
+    b = b3 + b1
+    if m.rbr_identity is not None:
+        idk = torch.zeros_like(k3)
+        input_dim = m.in_channels // m.groups
+        for i in range(m.in_channels):
+            idk[i, i % input_dim, 1, 1] = 1.0
+        kid, bid = fold_bn(idk, m.rbr_identity)
+        k, b = k + kid, b + bid
+    return k, b
+
+
+def act_of(mod):
+    if isinstance(mod, nn.SiLU):
+        return L.ACT_SILU, 0.0
+    if isinstance(mod, nn.LeakyReLU):
+        return L.ACT_LEAKY, float(mod.negative_slope)
+    if isinstance(mod, nn.Identity) or mod is None:
+        return L.ACT_NONE, 0.0
+    raise NotImplementedError(f"ycx: activation {type(mod).__name__} has no HIP epilogue")
+
+
+class Graph:
+    def __init__(self):
+        self.nodes = []
+
+    def add(self, kind, inputs, out, **p):
+        node = Node(kind, list(inputs), out, **p)
+        out.producer = node
+        for v in inputs:
+            v.consumers.append(node)
+        self.nodes.append(node)
+        return out
+
+    # ---- primitive ops ----
+    def conv(self, x: Val, w64, b64, k, s, p, act=(L.ACT_NONE, 0.0), residual=None, head=False):
+        cout, cin = int(w64.shape[0]), int(w64.shape[1])
+        if cin != x.c:
+            raise NotImplementedError(f"ycx: grouped/mismatched conv (cin {cin} vs input {x.c})")
+        ho, wo = (x.h + 2 * p - k) // s + 1, (x.w + 2 * p - k) // s + 1
+        out = Val(x.n, ho, wo, cout, role='output' if head else 'act')
+        ins = [x] + ([residual] if residual is not None else [])
+        kind = 'stem' if x.role == 'input' else 'conv'
+        if kind == 'stem' and residual is not None:
+            raise NotImplementedError("ycx: residual on the input conv")
+        return self.add(kind, ins, out, w=w64, b=b64, k=k, s=s, p=p, act=act[0], slope=act[1],
+                        residual=residual, ho=ho, wo=wo, layout=L.OUT_NCHW_F32 if head else L.OUT_NHWC)
+
+    def pool(self, x: Val, k, s, p):
+        if x.role == 'input':
+            raise NotImplementedError("ycx: pooling the raw input image")
+        ho, wo = (x.h + 2 * p - k) // s + 1, (x.w + 2 * p - k) // s + 1
+        return self.add('pool', [x], Val(x.n, ho, wo, x.c), k=k, s=s, p=p)
+
+    def upsample(self, x: Val):
+        return self.add('up', [x], Val(x.n, 2 * x.h, 2 * x.w, x.c))
+
+    def concat(self, xs):
+        n, h, w = xs[0].n, xs[0].h, xs[0].w
+        if any((v.n, v.h, v.w) != (n, h, w) for v in xs):
+            raise ValueError("ycx: Concat inputs differ in spatial size")
+        return self.add('concat', xs, Val(n, h, w, sum(v.c for v in xs)))
+
+
+def conv_module(g: Graph, m: Conv, x: Val, residual=None):
+    c = m.conv
+    if c.groups != 1 or _pair(c.dilation) != (1, 1):
+        raise NotImplementedError("ycx: grouped/dilated conv")
+    w, b = fold_bn(c.weight, m.bn)
+    return g.conv(x, w, b, _square(c.kernel_size, 'kernel'), _square(c.stride, 'stride'),
+                  _square(c.padding, 'padding'), act_of(m.act), residual=residual)
+
+
+def pool_module(g: Graph, mp: nn.MaxPool2d, x: Val):
+    if mp.ceil_mode or _pair(mp.dilation) != (1, 1):
+        raise NotImplementedError("ycx: ceil_mode / dilated max-pool")
+    k = _square(mp.kernel_size, 'pool kernel')
+    s = _square(mp.stride if mp.stride is not None else k, 'pool stride')
+    return g.pool(x, k, s, _square(mp.padding, 'pool padding'))
+
+
+def pyramid(g: Graph, x: Val, pools):
+    """SPP-style pools of x. s=1 'same' pools whose kernels step by 4 from 5
+    (5, 9, 13) run as a cascade of k=5 pools: maxpool_{a+b-1} = maxpool_a o maxpool_b
+    for stride 1 with -inf padding (exact, SPPF's own identity)."""
+    ks = [(_square(m.kernel_size, 'k'), _square(m.stride, 's'), _square(m.padding, 'p')) for m in pools]
+    cascade = all(s == 1 and p == k // 2 for k, s, p in ks) and [k for k, _, _ in ks] == [5 + 4 * i for i in range(len(ks))]
+    outs, cur = [], x
+    for (k, s, p), m in zip(ks, pools):
+        if cascade:
+            cur = g.pool(cur, 5, 1, 2)
+            outs.append(cur)
+        else:
+            outs.append(pool_module(g, m, x))
+    return outs
+
+
+def lower_module(g: Graph, m, x):
+    if isinstance(m, nn.Sequential):
+        for mm in m:
+            x = lower_module(g, mm, x)
+        return x
+    if isinstance(m, Conv):
+        return conv_module(g, m, x)
+    if isinstance(m, RepConv):
+        w, b = fold_repconv(m)
+        return g.conv(x, w, b, 3, m.stride, 1, act_of(m.act))
+    if isinstance(m, nn.Conv2d):
+        w = m.weight.detach().to('cpu', torch.float64)
+        b = m.bias.detach().to('cpu', torch.float64) if m.bias is not None else torch.zeros(w.shape[0],
+                                                                                            dtype=torch.float64)
+        if m.groups != 1:
+            raise NotImplementedError("ycx: grouped conv")
+        return g.conv(x, w, b, _square(m.kernel_size, 'k'), _square(m.stride, 's'), _square(m.padding, 'p'))
+    if isinstance(m, (MP, SP)):
+        return pool_module(g, m.m, x)
+    if isinstance(m, nn.MaxPool2d):
+        return pool_module(g, m, x)
+    if isinstance(m, Concat):
+        if m.d != 1:
+            raise NotImplementedError("ycx: Concat along a non-channel dim")
+        return g.concat(x)
+    if isinstance(m, nn.Upsample):
+        sf = m.scale_factor
+        sf = sf[0] if isinstance(sf, (tuple, list)) else sf
+        if m.mode != 'nearest' or m.size is not None or float(sf) != 2.0:
+            raise NotImplementedError("ycx: only nn.Upsample(None, 2, 'nearest') is supported")
+        return g.upsample(x)
+    if isinstance(m, nn.Identity):
+        return x
+    if isinstance(m, Bottleneck):
+        y = conv_module(g, m.cv1, x)
+        return conv_module(g, m.cv2, y, residual=x if m.add else None)
+    if isinstance(m, SPPCSPC):
+        x1 = conv_module(g, m.cv4, conv_module(g, m.cv3, conv_module(g, m.cv1, x)))
+        y1 = conv_module(g, m.cv6, conv_module(g, m.cv5, g.concat([x1] + pyramid(g, x1, list(m.m)))))
+        y2 = conv_module(g, m.cv2, x)
+        return conv_module(g, m.cv7, g.concat([y1, y2]))
+    if isinstance(m, SPPF):
+        x1 = conv_module(g, m.cv1, x)
+        y1 = pool_module(g, m.m, x1)
+        y2 = pool_module(g, m.m, y1)
+        y3 = pool_module(g, m.m, y2)
+        return conv_module(g, m.cv2, g.concat([x1, y1, y2, y3]))
+    if isinstance(m, SPP):
+        x1 = conv_module(g, m.cv1, x)
+        return conv_module(g, m.cv2, g.concat([x1] + pyramid(g, x1, list(m.m))))
+    if isinstance(m, BottleneckCSPA):
+        y1 = lower_module(g, m.m, conv_module(g, m.cv1, x))
+        return conv_module(g, m.cv3, g.concat([y1, conv_module(g, m.cv2, x)]))
+    if isinstance(m, BottleneckCSPB):
+        x1 = conv_module(g, m.cv1, x)
+        return conv_module(g, m.cv3, g.concat([lower_module(g, m.m, x1), conv_module(g, m.cv2, x1)]))
+    if isinstance(m, BottleneckCSPC):
+        y1 = conv_module(g, m.cv3, lower_module(g, m.m, conv_module(g, m.cv1, x)))
+        return conv_module(g, m.cv4, g.concat([y1, conv_module(g, m.cv2, x)]))
+    if isinstance(m, Detect):
+        outs = []
+        for conv, idx in m.heads_in_output_order():
+            w = conv.weight.detach().to('cpu', torch.float64)
+            b = conv.bias.detach().to('cpu', torch.float64)
+            outs.append(g.conv(x[idx], w, b, 1, 1, 0, head=True))
+        return outs
+    if isinstance(m, IDetect):
+        outs = []
+        for i in range(m.nl):
+            conv = m.m[i]
+            # x_i = im * (conv(x_i + ia)) = (im*W) x + im*(b + W.ia)   (nets/idetect.py:30-31)
+            w = conv.weight.detach().to('cpu', torch.float64)
+            b = conv.bias.detach().to('cpu', torch.float64)
+            ia = m.ia[i].implicit.detach().to('cpu', torch.float64).reshape(-1)
+            im = m.im[i].implicit.detach().to('cpu', torch.float64).reshape(-1)
+            b = (b + w[:, :, 0, 0] @ ia) * im
+            w = w * im.reshape(-1, 1, 1, 1)
+            outs.append(g.conv(x[i], w, b, 1, 1, 0, head=True))
+        return outs
+    raise NotImplementedError(f"ycx: no HIP lowering for {type(m).__name__}")
+
+
+class Plan:
+    """Device-independent lowering of a Model for one input shape: the graph
+    after all passes, its outputs and its algorithmic FLOPs."""
+
+    def __init__(self, model, shape):
+        if len(shape) != 4:
+            raise ValueError(f"ycx: expected an NCHW input, got shape {shape}")
+        self.shape = tuple(int(s) for s in shape)
+        n, c, h, w = self.shape
+        g = Graph()
+        self.input_val = Val(n, h, w, c, role='input')
+        ys, x = [], self.input_val
+        for m in model.model:  # nets/yolo.py:145-151
+            if m.f != -1:
+                x = ys[m.f] if isinstance(m.f, int) else [x if j == -1 else ys[j] for j in m.f]
+            x = lower_module(g, m, x)
+            ys.append(x)
+        self.is_list = isinstance(x, list)
+        self.out_vals = list(x) if self.is_list else [x]
+        self.graph = g
+        self._passes()
+
+    @property
+    def conv_flops(self):
+        """Algorithmic FLOPs: sum of 2*N*Ho*Wo*Cout*Cin*k*k over the folded convs."""
+        return sum(2 * nd.inputs[0].n * nd.p['ho'] * nd.p['wo'] * int(nd.p['w'].shape[0]) * int(nd.p['w'].shape[1])
+                   * nd.p['k'] ** 2 for nd in self.graph.nodes if nd.kind in ('conv', 'stem'))
+
+    def counts(self):
+        c = {}
+        for nd in self.graph.nodes:
+            kind = nd.kind
+            if kind == 'concat':
+                c['copy'] = c.get('copy', 0) + len(nd.p['copies'])
+            c[kind] = c.get(kind, 0) + 1
+        return c
+
+    def _passes(self):
+        g = self.graph
+        for v in self.out_vals:
+            if v.role != 'output':  # not a head conv: convert NHWC -> fp32 NCHW at the end
+                o = Val(v.n, v.h, v.w, v.c, role='output')
+                g.add('tonchw', [v], o)
+                self.out_vals[self.out_vals.index(v)] = o
+        # Fuse nearest-x2 upsample into the producing conv's store.
+        keep = []
+        for node in g.nodes:
+            if node.kind == 'up':
+                v = node.inputs[0]
+                prod = v.producer
+                if prod is not None and prod.kind == 'conv' and len(v.consumers) == 1 and v.role == 'act':
+                    prod.out = node.out
+                    prod.p['layout'] = L.OUT_NHWC_UP2
+                    node.out.producer = prod
+                    continue
+            keep.append(node)
+        g.nodes = keep
+        # Concat: producers write their channel slice directly when they can.
+        for node in g.nodes:
+            if node.kind != 'concat':
+                continue
+            out = node.out
+            out.buf = Buf(out.n, out.h, out.w, out.c)
+            copies, off = [], 0
+            for v in node.inputs:
+                if v.buf is None and v.role == 'act' and v.producer is not None and \
+                        v.producer.kind in ('conv', 'stem', 'pool', 'up'):
+                    v.buf, v.coff = out.buf, off
+                else:
+                    copies.append((v, off))
+                off += v.c
+            node.p['copies'] = copies
+        for node in g.nodes:
+            v = node.out
+            if v.buf is None and v.role == 'act':
+                v.buf = Buf(v.n, v.h, v.w, v.c)
+
+
+class Engine:
+    """A compiled plan bound to device memory for one (input shape, device, precision)."""
+
+    def __init__(self, model, shape, device, precision='bf16'):
+        if device.type != 'cuda':
+            raise RuntimeError("ycx: the HIP path needs the model input on a ROCm device (tensor.to('cuda')); "
+                               "there is no CPU path")
+        self.plan = Plan(model, shape)
+        self.shape, self.device, self.precision = self.plan.shape, device, precision
+        self.dtype = torch.bfloat16 if precision == 'bf16' else torch.float32
+        self.dt = L.DT_BF16 if precision == 'bf16' else L.DT_F32
+        self.graph_exec = None
+        self.graph, self.out_vals, self.is_list = self.plan.graph, self.plan.out_vals, self.plan.is_list
+        self._build()
+
+    def _cout_pad(self, cout):
+        if self.dt == L.DT_F32:
+            return -(-cout // 64) * 64
+        if cout <= 32:
+            return 32
+        if cout <= 64:
+            return 64
+        return -(-cout // 128) * 128
+
+    def _build(self):
+        dev, dt = self.device, self.dtype
+        self.buffers, self.params = [], []
+        seen = set()
+        for node in self.graph.nodes:
+            for v in [node.out] + node.inputs:
+                b = v.buf
+                if b is not None and id(b) not in seen:
+                    seen.add(id(b))
+                    b.tensor = torch.empty((b.n, b.h, b.w, b.c), dtype=dt, device=dev)
+                    self.buffers.append(b.tensor)
+        ops, self.input_slots, self.output_slots, self.op_info = [], [], {}, []
+        self.conv_flops = 0
+        for node in self.graph.nodes:
+            k = node.kind
+            if k in ('conv', 'stem'):
+                ops.append(self._conv_op(node))
+            elif k == 'pool':
+                ops.append(self._pool_op(node))
+            elif k == 'up':
+                ops.append(self._copy_op(node.inputs[0], node.out, 0, scale=2))
+            elif k == 'concat':
+                for v, off in node.p['copies']:
+                    ops.append(self._copy_op(v, node.out, off, scale=1))
+            elif k == 'tonchw':
+                ops.append(self._copy_op(node.inputs[0], node.out, 0, scale=1, nchw=True))
+            else:
+                raise AssertionError(k)
+        self.n_ops = len(ops)
+        self.ops = (L.Op * max(1, self.n_ops))(*ops)
+        self.fixed_outputs = None
+
+    def _val_ptr(self, v, op_index, field):
+        if v.role == 'input':
+            self.input_slots.append((op_index, field))
+            return None
+        if v.role == 'output':
+            self.output_slots.setdefault(id(v), []).append((op_index, field))
+            return None
+        return v.buf.tensor.data_ptr()
+
+    def _conv_op(self, node):
+        p, x, out = node.p, node.inputs[0], node.out
+        w64, b64 = p['w'], p['b']
+        cout, cin, k = int(w64.shape[0]), int(w64.shape[1]), p['k']
+        stem = node.kind == 'stem'
+        cpad = self._cout_pad(cout)
+        wp = torch.zeros((cpad, cin, k, k), dtype=torch.float64)
+        wp[:cout] = w64
+        bp = torch.zeros(cpad, dtype=torch.float64)
+        bp[:cout] = b64
+        if stem:  # [kh][kw][cin][cout_pad] fp32
+            wt = wp.permute(2, 3, 1, 0).contiguous().to(torch.float32)
+        else:     # [cout_pad][kh][kw][cin] in the activation dtype
+            wt = wp.permute(0, 2, 3, 1).contiguous().to(self.dtype)
+        wt = wt.to(self.device)
+        bt = bp.to(torch.float32).to(self.device)
+        self.params += [wt, bt]
+        d = L.ConvDesc()
+        d.n, d.h, d.w, d.cin = x.n, x.h, x.w, cin
+        if x.role == 'input':
+            d.in_c_off, d.in_c_stride = 0, x.c
+        else:
+            d.in_c_off, d.in_c_stride = x.coff, x.buf.c
+        d.ho, d.wo, d.cout, d.cout_pad = p['ho'], p['wo'], cout, cpad
+        d.kh = d.kw = k
+        d.stride, d.pad, d.act, d.leaky_slope = p['s'], p['p'], p['act'], p['slope']
+        d.dtype, d.out_layout = self.dt, p['layout']
+        if p['layout'] == L.OUT_NCHW_F32:
+            d.out_c_off, d.out_c_stride = 0, cout
+        else:
+            d.out_c_off, d.out_c_stride = out.coff, out.buf.c
+        r = p['residual']
+        if r is not None:
+            d.res_c_off, d.res_c_stride = r.coff, r.buf.c
+        d.tile = 0
+        op = L.Op()
+        op.kind = L.OP_STEM if stem else L.OP_CONV
+        op.d.conv = d
+        idx = len(self.op_info)
+        op.in_ = self._val_ptr(x, idx, 'in_')
+        op.weight, op.bias = wt.data_ptr(), bt.data_ptr()
+        op.out = self._val_ptr(out, idx, 'out')
+        op.residual = r.buf.tensor.data_ptr() if r is not None else None
+        flops = 2 * x.n * p['ho'] * p['wo'] * cout * cin * k * k
+        self.conv_flops += flops
+        tile = 0 if stem else int(L.lib.ycx_conv_pick_tile(ctypes.byref(d)))
+        name = 'stem' if stem else L.lib.ycx_conv_tile_name(tile).decode()
+        self.op_info.append(dict(kind=node.kind, name=name, flops=flops,
+                                 shape=(x.n, x.h, x.w, cin, cout, k, p['s'])))
+        return op
+
+    def _pool_op(self, node):
+        x, out, p = node.inputs[0], node.out, node.p
+        d = L.PoolDesc()
+        d.n, d.h, d.w, d.c, d.in_c_off, d.in_c_stride = x.n, x.h, x.w, x.c, x.coff, x.buf.c
+        d.ho, d.wo, d.out_c_off, d.out_c_stride = out.h, out.w, out.coff, out.buf.c
+        d.k, d.stride, d.pad, d.dtype = p['k'], p['s'], p['p'], self.dt
+        op = L.Op()
+        op.kind = L.OP_POOL
+        op.d.pool = d
+        op.in_, op.out = x.buf.tensor.data_ptr(), out.buf.tensor.data_ptr()
+        self.op_info.append(dict(kind='pool', name=f"maxpool_k{p['k']}s{p['s']}", flops=0,
+                                 bytes=(x.n * (x.h * x.w + out.h * out.w) * x.c * self.dtype.itemsize)))
+        return op
+
+    def _copy_op(self, x, out, off, scale, nchw=False):
+        d = L.CopyDesc()
+        d.n, d.h, d.w, d.c, d.in_c_off, d.in_c_stride = x.n, x.h, x.w, x.c, x.coff, x.buf.c
+        d.scale, d.dtype = scale, self.dt
+        op = L.Op()
+        op.kind = L.OP_COPY
+        idx = len(self.op_info)
+        op.in_ = x.buf.tensor.data_ptr()
+        if nchw:
+            d.out_c_off, d.out_c_stride, d.out_layout = 0, x.c, L.OUT_NCHW_F32
+            op.out = self._val_ptr(out, idx, 'out')
+        else:
+            d.out_c_off, d.out_c_stride, d.out_layout = off, out.buf.c, L.OUT_NHWC
+            op.out = out.buf.tensor.data_ptr()
+        op.d.copy = d
+        self.op_info.append(dict(kind='copy', name='upsample2x' if scale == 2 else 'copy', flops=0))
+        return op
+
+    # ------------------------------------------------------------------
+    def _alloc_outputs(self):
+        outs = []
+        for v in self.out_vals:
+            t = torch.empty((v.n, v.c, v.h, v.w), dtype=torch.float32, device=self.device)
+            for idx, field in self.output_slots.get(id(v), []):
+                setattr(self.ops[idx], field, t.data_ptr())
+            outs.append(t)
+        return outs
+
+    def _bind_input(self, x):
+        if x.device != self.device or x.dtype != torch.float32 or not x.is_contiguous():
+            x = x.to(self.device, torch.float32).contiguous()
+        if tuple(x.shape) != self.shape:
+            raise ValueError(f"ycx: engine built for {self.shape}, got {tuple(x.shape)}")
+        for idx, field in self.input_slots:
+            setattr(self.ops[idx], field, x.data_ptr())
+        return x
+
+    def _result(self, outs):
+        return outs if self.is_list else outs[0]
+
+    def run(self, x, events=None):
+        """Eager forward: fresh output tensors every call (like the reference)."""
+        x = self._bind_input(x)
+        outs = self._alloc_outputs()
+        ev = None
+        if events is not None:
+            ev = (ctypes.c_void_p * (self.n_ops + 1))(*[e.cuda_event for e in events])
+        stream = L.stream_handle(self.device)
+        L.check(L.lib.ycx_run_ops(self.ops, self.n_ops, stream, ev), "ycx_run_ops")
+        return self._result(outs)
+
+    # ---- static-I/O path for benchmarking / serving loops ----
+    def bind_static(self, x):
+        """Pin the plan to persistent input/output tensors (required by capture())."""
+        self.static_input = self._bind_input(x)
+        self.fixed_outputs = self._alloc_outputs()
+        return self.static_input, self._result(self.fixed_outputs)
+
+    def run_static(self, events=None):
+        ev = None
+        if events is not None:
+            ev = (ctypes.c_void_p * (self.n_ops + 1))(*[e.cuda_event for e in events])
+        L.check(L.lib.ycx_run_ops(self.ops, self.n_ops, L.stream_handle(self.device), ev), "ycx_run_ops")
+        return self._result(self.fixed_outputs)
+
+    def capture(self):
+        """Capture the static plan into a HIP graph (one launch per forward)."""
+        if self.fixed_outputs is None:
+            raise RuntimeError("ycx: call bind_static() before capture()")
+        if self.graph_exec is None:
+            h = ctypes.c_void_p()
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            L.check(L.lib.ycx_graph_capture(self.ops, self.n_ops, s.cuda_stream, ctypes.byref(h)),
+                    "ycx_graph_capture")
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self.graph_exec = h.value
+        return self.graph_exec
+
+    def replay(self):
+        L.check(L.lib.ycx_graph_launch(self.graph_exec, L.stream_handle(self.device)), "ycx_graph_launch")
+        return self._result(self.fixed_outputs)
+
+    def close(self):
+        if self.graph_exec is not None:
+            L.lib.ycx_graph_destroy(self.graph_exec)
+            self.graph_exec = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- introspection ----
+    @property
+    def flops_per_image(self):
+        return self.conv_flops / self.shape[0]
+
+    def summary(self):
+        kinds = {}
+        for info in self.op_info:
+            kinds[info['kind']] = kinds.get(info['kind'], 0) + 1
+        mem = sum(t.numel() * t.element_size() for t in self.buffers)
+        return dict(ops=self.n_ops, kinds=kinds, activation_bytes=mem, gflop_per_image=self.flops_per_image / 1e9)

@@ -1,0 +1,225 @@
+"""YOLO model builder and the drop-in ``Model`` (nets/yolo.py semantics).
+
+``parse_model`` restates the reference builder (nets/yolo.py:15-87): channel
+bookkeeping ``c2 = make_divisible(c2 * width_multiple, 8)``, depth gain, repeat
+insertion for CSP-type blocks, concat channel sums, head channel lists and the
+save list. Unlike the reference it never calls ``eval`` on YAML strings: module
+names come from a whitelist and arguments from a small safe parser
+(``None``, ``nc``/``num_classes``, ``anchors``, ``nn.LeakyReLU(0.1)``,
+``nn.SiLU()``, literals), SURVEY.md Appendix B.10.
+
+``Model.forward`` runs inference only, through the HIP engine (``ycx.engine``):
+the first call for a given (input shape, device, precision) lowers the module
+tree to a static op plan with BN/RepConv folded and buffers pre-allocated.
+Training is out of scope: ``forward`` in train mode raises.
+"""
+from __future__ import annotations
+
+import ast
+import math
+import re
+from copy import deepcopy
+from enum import Enum
+
+import torch
+from torch import nn
+
+from ..utils.helper_io import cvt_cfg
+from .common import (SP, SPP, SPPCSPC, SPPF, MP, Bottleneck, BottleneckCSPA, BottleneckCSPB, BottleneckCSPC,
+                     Concat, Conv, ImplicitA, ImplicitM, RepConv)
+from .detect import Detect, IDetect
+
+
+def make_divisible(x, divisor):
+    return math.ceil(x / divisor) * divisor
+
+
+_MODULES = {
+    'Conv': Conv, 'MP': MP, 'SP': SP, 'Concat': Concat, 'SPPCSPC': SPPCSPC, 'RepConv': RepConv,
+    'Bottleneck': Bottleneck, 'BottleneckCSPA': BottleneckCSPA, 'BottleneckCSPB': BottleneckCSPB,
+    'BottleneckCSPC': BottleneckCSPC, 'SPP': SPP, 'SPPF': SPPF, 'ImplicitA': ImplicitA,
+    'ImplicitM': ImplicitM, 'Detect': Detect, 'IDetect': IDetect,
+    'nn.Conv2d': nn.Conv2d, 'nn.BatchNorm2d': nn.BatchNorm2d, 'nn.Upsample': nn.Upsample,
+}
+# Reference modules constructible by its parse_model but used by neither shipped
+# YAML: named here so the error says "out of scope", not "unknown".
+_OUT_OF_SCOPE = {
+    'ReOrg', 'Chuncat', 'Shortcut', 'Foldcut', 'RobustConv', 'RobustConv2', 'GhostConv', 'Stem', 'DownC',
+    'Res', 'ResX', 'Ghost', 'GhostSPPCSPC', 'GhostStem', 'dw_conv', 'Focus', 'Contract', 'Expand', 'Classify',
+    'TransformerLayer', 'TransformerBlock', 'IAuxDetect', 'IBin', 'RepBottleneck',
+} | {f'{p}{s}' for p in ('Res', 'ResX', 'RepRes', 'RepResX', 'Ghost', 'RepBottleneck')
+     for s in ('CSPA', 'CSPB', 'CSPC')}
+
+_CONV_LIKE = (nn.Conv2d, Conv, RepConv, SPP, SPPF, SPPCSPC, Bottleneck, BottleneckCSPA, BottleneckCSPB,
+              BottleneckCSPC)
+_CSP_LIKE = (SPPCSPC, BottleneckCSPA, BottleneckCSPB, BottleneckCSPC)
+_ACTS = {'LeakyReLU': nn.LeakyReLU, 'SiLU': nn.SiLU, 'Identity': nn.Identity}
+_CALL_RE = re.compile(r'^(?:nn\.)?(\w+)\((.*)\)$')
+
+
+def _resolve_module(m):
+    if not isinstance(m, str):
+        return m
+    if m in _MODULES:
+        return _MODULES[m]
+    base = m.split('.')[-1]
+    if base in _OUT_OF_SCOPE or m in _OUT_OF_SCOPE:
+        raise NotImplementedError(f"ycx: module '{m}' is out of scope for the HIP inference path (SURVEY.md §2)")
+    raise ValueError(f"ycx: unknown module '{m}' in network config")
+
+
+def _resolve_arg(a, nc, anchors):
+    if not isinstance(a, str):
+        return a
+    if a == 'None':
+        return None
+    if a in ('nc', 'num_classes'):
+        return nc
+    if a == 'anchors':
+        return anchors
+    mt = _CALL_RE.match(a.strip())
+    if mt and mt.group(1) in _ACTS:
+        inner = mt.group(2).strip()
+        params = [ast.literal_eval(p.strip()) for p in inner.split(',')] if inner else []
+        return _ACTS[mt.group(1)](*params)
+    try:
+        return ast.literal_eval(a)
+    except (ValueError, SyntaxError):
+        return a  # e.g. 'nearest' (the reference's eval fails and keeps the string too)
+
+
+def parse_model(d, ch, anchors, num_classes):
+    """Network dict -> (nn.Sequential of layer modules tagged .i/.f/.type/.np, save list)."""
+    nc, gd, gw = num_classes, d['depth_multiple'], d['width_multiple']
+    na = (len(anchors[0]) // 2) if isinstance(anchors, list) else anchors
+    no = na * (nc + 5)
+    layers, save, c2 = [], [], ch[-1]
+    for i, (f, n, m, args) in enumerate(d['backbone'] + d['head']):
+        m = _resolve_module(m)
+        args = [_resolve_arg(a, nc, anchors) for a in args]
+        n = max(round(n * gd), 1) if n > 1 else n
+        if m in _CONV_LIKE:
+            c1, c2 = ch[f], args[0]
+            if c2 != no:
+                c2 = make_divisible(c2 * gw, 8)
+            args = [c1, c2, *args[1:]]
+            if m in _CSP_LIKE:
+                args.insert(2, n)
+                n = 1
+        elif m is nn.BatchNorm2d:
+            args = [ch[f]]
+        elif m is Concat:
+            c2 = sum(ch[x] for x in f)
+        elif m in (Detect, IDetect):
+            args.append([ch[x] for x in f])
+            if isinstance(args[1], int):
+                args[1] = [list(range(args[1] * 2))] * len(f)
+        else:
+            c2 = ch[f]
+        m_ = nn.Sequential(*[m(*args) for _ in range(n)]) if n > 1 else m(*args)
+        m_.i, m_.f = i, f
+        m_.type = f"{m.__module__}.{m.__name__}"
+        m_.np = sum(x.numel() for x in m_.parameters())
+        save.extend(x % i for x in ([f] if isinstance(f, int) else f) if x != -1)
+        layers.append(m_)
+        if i == 0:
+            ch = []
+        ch.append(c2)
+    return nn.Sequential(*layers), sorted(save)
+
+
+class WeightInitial(Enum):
+    NA = 0
+    Random = 1
+
+
+PRECISIONS = ('bf16', 'f32')
+
+
+class Model(nn.Module):
+    """Drop-in for nets/yolo.py ``Model`` (constructor :95-112, forward :143-153).
+
+    forward(x: fp32 [N, C, H, W] on a ROCm device) -> the last layer's output:
+    ``[P5, P4, P3]`` fp32 NCHW logits for a Detect head (nets/detect.py:38).
+    ``precision`` selects the kernel dtype: 'bf16' (default, MFMA bf16, fp32
+    accumulate) or 'f32' (parity mode, exact-fp32 MFMA).
+    """
+
+    def __init__(self, model_cfg, anchors, num_classes, image_chan=3, weight_initial=WeightInitial.Random,
+                 precision='bf16'):
+        super().__init__()
+        self.traced = False
+        self.weight_initial = weight_initial
+        self.anchors = anchors
+        self.num_classes = num_classes
+        self.image_chan = image_chan
+        self.model, self.save = parse_model(deepcopy(cvt_cfg(model_cfg)), ch=[image_chan], anchors=anchors,
+                                            num_classes=num_classes)
+        self.set_precision(precision)
+        self.initial_weights()
+
+    # ---- reference API -------------------------------------------------
+    def initial_weights(self):
+        """nets/yolo.py:114-125: conv/linear W ~ N(0, 0.02); BN gamma ~ N(1, 0.02), beta = 0."""
+        if self.weight_initial == WeightInitial.NA:
+            return
+        for m in self.modules():
+            if isinstance(m, (nn.Conv2d, nn.Linear)):
+                nn.init.normal_(m.weight, 0, 0.02)
+            elif isinstance(m, (nn.BatchNorm2d, nn.GroupNorm)):
+                nn.init.normal_(m.weight, 1.0, 0.02)
+                nn.init.constant_(m.bias, 0)
+            elif isinstance(m, (nn.Hardswish, nn.LeakyReLU, nn.ReLU, nn.ReLU6)):
+                m.inplace = True
+        self.invalidate()
+
+    def print_info(self):
+        n_p = sum(x.numel() for x in self.parameters())
+        n_g = sum(x.numel() for x in self.parameters() if x.requires_grad)
+        print('{0:5s} {1:40s} {2:9s} {3:12s} {4:20s} {5:10s} {6:10s}'.format(
+            'layer', 'name', 'gradient', 'parameters', 'shape', 'mu', 'sigma'))
+        for i, (name, p) in enumerate(self.named_parameters()):
+            print('%5g %40s %9s %12g %20s %10.3g %10.3g' % (i, name, p.requires_grad, p.numel(), list(p.shape),
+                                                            p.mean(), p.std()))
+        print('total parameters: {0:7g} total gradients: {1:7g}'.format(n_p, n_g))
+
+    def forward(self, x):
+        if self.training:
+            raise RuntimeError("ycx: Model is inference-only on the HIP path (training is out of scope); "
+                               "call .eval() first")
+        return self.engine_for(x.shape, x.device).run(x)
+
+    # ---- engine management --------------------------------------------
+    def set_precision(self, precision):
+        if precision not in PRECISIONS:
+            raise ValueError(f"ycx: precision must be one of {PRECISIONS}, got {precision!r}")
+        self.precision = precision
+        self.invalidate()
+        return self
+
+    def invalidate(self):
+        """Drop compiled plans (packed weights); called when parameters change."""
+        for eng in getattr(self, '_engines', {}).values():
+            eng.close()
+        self._engines = {}
+
+    def engine_for(self, shape, device):
+        from ..engine import Engine
+        shape = tuple(int(s) for s in shape)
+        dev = torch.device(device)
+        key = (shape, str(dev), self.precision)
+        eng = self._engines.get(key)
+        if eng is None:
+            eng = Engine(self, shape, dev, self.precision)
+            self._engines[key] = eng
+        return eng
+
+    def load_state_dict(self, state_dict, strict=True, *args, **kwargs):
+        r = super().load_state_dict(state_dict, strict, *args, **kwargs)
+        self.invalidate()
+        return r
+
+    def _apply(self, fn, *args, **kwargs):
+        r = super()._apply(fn, *args, **kwargs)
+        self.invalidate()
+        return r
