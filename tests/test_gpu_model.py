@@ -74,7 +74,7 @@ def test_engine_plan_properties(device):
     eng = m.engine_for((2, 3, 640, 640), device)
     s = eng.summary()
     assert s['kinds'].get('copy', 0) == 0, "every concat input should alias its slice (no copy kernels)"
-    assert s['kinds']['conv'] + s['kinds']['stem'] == 93  # 95 convs - 2 RepConv 1x1 branches folded... see DESIGN
+    assert s['kinds']['conv'] + s['kinds']['stem'] == 92  # 95 convs minus the 3 folded RepConv 1x1 branches
     assert abs(s['gflop_per_image'] - 104.511078400) < 1e-6
 
 
