@@ -82,16 +82,30 @@ def test_nms_edge_cases(device):
     pred[0, 3, 5], pred[0, 3, 6] = 0.0, 1.0  # row 3 -> class 1
     _, keep, kc = nms_device(pred.clone(), 2, 0.25, 0.5)
     assert int(kc[0]) == 2 and keep[0, :2].tolist() == [0, 3]
-    # every row passes (dense worst case, > LDS key capacity path at 16384 rows)
-    g = torch.Generator().manual_seed(0)
-    pred = torch.rand(1, 16384, 8, generator=g)
-    pred[..., 2:4] *= 0.05
-    pred[..., 4] = 0.5 + 0.5 * pred[..., 4]
-    pred = pred.to(device)
-    ref_keep, _ = ref_post.nms_keep_rows(pred.cpu().clone(), 3, 0.0, 0.3)
-    _, keep, kc = nms_device(pred.clone(), 3, 0.0, 0.3)
-    k = int(kc[0])
-    np.testing.assert_array_equal(keep[0, :k].cpu().numpy(), ref_keep[0].numpy())
+    # the '>' boundary: a threshold equal to the fp32 IoU keeps both boxes, the
+    # next double below suppresses (also exercises the division-free compare)
+    pred = torch.zeros(1, 2, 6, device=device)
+    pred[0, 0, :4] = torch.tensor([5.0, 5.0, 10.0, 10.0])   # xywh -> xyxy (0, 0, 10, 10)
+    pred[0, 1, :4] = torch.tensor([5.5, 5.5, 10.0, 10.0])   # -> (0.5, 0.5, 10.5, 10.5)
+    pred[0, :, 4] = torch.tensor([0.9, 0.8])
+    pred[0, :, 5] = 1.0
+    inter, a0, a1 = np.float32(90.25), np.float32(100.0), np.float32(100.0)
+    iou = float(inter / (a0 + a1 - inter))
+    for thr, want in ((iou, 2), (np.nextafter(iou, 0.0), 1), (np.nextafter(iou, 1.0), 2)):
+        _, keep, kc = nms_device(pred.clone(), 1, 0.1, thr)
+        assert int(kc[0]) == want, (thr, int(kc[0]))
+    # every row passes (the conf_thres=0.001 evaluation regime): 3 classes of
+    # ~5.5k (bitmask path, LDS sort) and one class of 16384 (workspace sort)
+    for nc in (3, 1):
+        g = torch.Generator().manual_seed(nc)
+        pred = torch.rand(1, 16384, 5 + nc, generator=g)
+        pred[..., 2:4] *= 0.05
+        pred[..., 4] = 0.5 + 0.5 * pred[..., 4]
+        pred = pred.to(device)
+        ref_keep, _ = ref_post.nms_keep_rows(pred.cpu().clone(), nc, 0.0, 0.3)
+        _, keep, kc = nms_device(pred.clone(), nc, 0.0, 0.3)
+        k = int(kc[0])
+        np.testing.assert_array_equal(keep[0, :k].cpu().numpy(), ref_keep[0].numpy())
 
 
 @pytest.mark.parametrize('precision', ['f32', 'bf16'])

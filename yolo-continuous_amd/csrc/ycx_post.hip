@@ -1,13 +1,10 @@
-// Post-processing of the YOLO heads on gfx950: box decode, candidate filter,
-// per-image sort and per-class greedy NMS.
+// Post-processing of the YOLO heads on gfx950: box decode and candidate filter
+// (the sort + per-class NMS that consumes the candidates is in ycx_nms.hip).
 //
 //   ycx_decode          decode_box, one level              detect.py:29-87
 //   ycx_filter_decoded  non_max_suppression :98-121         (xyxy in place, class max,
 //                                                            obj*cls_conf >= conf_thres)
 //   ycx_decode_filter   the two above fused, reading raw heads (fast path)
-//   ycx_sort_nms        the per-class torchvision.ops.nms loop (detect.py:124-137):
-//                       one workgroup per image, 64-bit key bitonic sort in LDS,
-//                       greedy suppression with an LDS bitset
 //
 // Bit-exactness: the float expressions and their evaluation order restate the
 // reference (and torchvision's CPU nms kernel) operation by operation; FMA
@@ -173,145 +170,6 @@ __global__ void __launch_bounds__(256) decode_filter_kernel(DecodeFilterArgs a, 
   }
 }
 
-// ---------------------------------------------------------------------------
-// Sort + NMS: one 1024-thread workgroup per image.
-// ---------------------------------------------------------------------------
-constexpr int kNmsThreads = 1024;
-constexpr int kLdsKeys = 8192;  // 64 KiB of 64-bit keys; larger sets sort in the workspace
-
-struct NmsLayout {
-  size_t keys_off, box_off, area_off, per_image;
-  int p_max;
-};
-
-__host__ __device__ inline int next_pow2(int v) {
-  int p = 1;
-  while (p < v) p <<= 1;
-  return p;
-}
-__host__ __device__ inline int row_bits(int rows) {
-  int b = 1;
-  while ((1 << b) < rows) ++b;
-  return b;
-}
-__host__ __device__ inline NmsLayout nms_layout(int rows_total) {
-  NmsLayout L;
-  L.p_max = next_pow2(rows_total);
-  L.keys_off = 0;
-  L.box_off = (size_t)L.p_max * 8;
-  L.area_off = L.box_off + (size_t)rows_total * 16;
-  L.per_image = (L.area_off + (size_t)rows_total * 4 + 255) & ~(size_t)255;
-  return L;
-}
-
-__device__ void bitonic_sort(unsigned long long* keys, int P) {
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < P; i += blockDim.x) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const unsigned long long x = keys[i], y = keys[ixj];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) { keys[i] = y; keys[ixj] = x; }
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-__global__ void __launch_bounds__(kNmsThreads) sort_nms_kernel(ycx_nms_desc d, const ycx_cand* __restrict__ cand,
-                                                               const int* __restrict__ cand_rows,
-                                                               const int* __restrict__ cand_counts, char* ws,
-                                                               float* __restrict__ dets, int* __restrict__ keep_rows,
-                                                               int* __restrict__ keep_counts) {
-  __shared__ unsigned long long s_keys[kLdsKeys];
-  __shared__ unsigned int s_removed[(kLdsKeys * 16) / 32];  // bitset for up to 131072 candidates
-  const int img = blockIdx.x;
-  const int tid = threadIdx.x;
-  const NmsLayout L = nms_layout(d.rows_total);
-  char* wsi = ws + (size_t)img * L.per_image;
-  const int cnt = min(cand_counts[img], d.rows_total);
-  const int rb = row_bits(d.rows_total);
-  const ycx_cand* ci = cand + (size_t)img * d.rows_total;
-  const int* cr = cand_rows + (size_t)img * d.rows_total;
-
-  const int P = next_pow2(max(cnt, 1));
-  unsigned long long* keys = P <= kLdsKeys ? s_keys : reinterpret_cast<unsigned long long*>(wsi + L.keys_off);
-  for (int i = tid; i < P; i += blockDim.x) {
-    unsigned long long k = ~0ull;
-    if (i < cnt) {
-      const int r = cr[i];
-      const ycx_cand c = ci[r];
-      const float score = c.obj * c.cls_conf;
-      const unsigned int inv = 0xFFFFFFFFu - __float_as_uint(score);
-      k = ((unsigned long long)(unsigned)c.cls << (32 + rb)) | ((unsigned long long)inv << rb) |
-          (unsigned long long)(unsigned)r;
-    }
-    keys[i] = k;
-  }
-  const int nwords = (cnt + 31) >> 5;
-  for (int i = tid; i < nwords; i += blockDim.x) s_removed[i] = 0u;
-  __syncthreads();
-  bitonic_sort(keys, P);
-
-  // Gather sorted boxes + areas (areas = (x2-x1)*(y2-y1), torchvision nms).
-  f32x4* sbox = reinterpret_cast<f32x4*>(wsi + L.box_off);
-  float* sarea = reinterpret_cast<float*>(wsi + L.area_off);
-  const unsigned long long rmask = (1ull << rb) - 1ull;
-  for (int i = tid; i < cnt; i += blockDim.x) {
-    const ycx_cand c = ci[(int)(keys[i] & rmask)];
-    sbox[i] = f32x4{c.x1, c.y1, c.x2, c.y2};
-    sarea[i] = (c.x2 - c.x1) * (c.y2 - c.y1);
-  }
-  __syncthreads();
-
-  // Greedy per-class suppression in sorted order (class asc, score desc).
-  int nkeep = 0;
-  int i = 0;
-  while (true) {
-    // Skip to the next unsuppressed candidate (uniform: every lane reads the same words).
-    while (i < cnt) {
-      const unsigned int free_bits = ~s_removed[i >> 5] >> (i & 31);
-      if (free_bits) { i += __builtin_ctz(free_bits); break; }
-      i = (i | 31) + 1;
-    }
-    if (i >= cnt) break;
-    const unsigned long long ki = keys[i];
-    const int row_i = (int)(ki & rmask);
-    if (nkeep < d.max_det && tid == 0) {
-      const ycx_cand c = ci[row_i];
-      float* o = dets + ((size_t)img * d.max_det + nkeep) * 7;
-      o[0] = c.x1; o[1] = c.y1; o[2] = c.x2; o[3] = c.y2;
-      o[4] = c.obj; o[5] = c.cls_conf; o[6] = (float)c.cls;
-      keep_rows[(size_t)img * d.max_det + nkeep] = row_i;
-    }
-    ++nkeep;
-    const unsigned long long cls_i = ki >> (32 + rb);
-    const f32x4 bi = sbox[i];
-    const float ai = sarea[i];
-    for (int j = i + 1 + tid; j < cnt; j += blockDim.x) {
-      if ((keys[j] >> (32 + rb)) != cls_i) break;  // sorted by class: the segment ended
-      if ((s_removed[j >> 5] >> (j & 31)) & 1u) continue;
-      const f32x4 bj = sbox[j];
-      const float xx1 = fmaxf(bi[0], bj[0]), yy1 = fmaxf(bi[1], bj[1]);
-      const float xx2 = fminf(bi[2], bj[2]), yy2 = fminf(bi[3], bj[3]);
-      const float w = fmaxf(0.0f, xx2 - xx1), h = fmaxf(0.0f, yy2 - yy1);
-      const float inter = w * h;
-      const float ovr = inter / (ai + sarea[j] - inter);
-      if ((double)ovr > d.iou_thres) atomicOr(&s_removed[j >> 5], 1u << (j & 31));
-    }
-    __syncthreads();
-    ++i;
-  }
-  if (tid == 0) keep_counts[img] = nkeep;
-  for (int k = nkeep + tid; k < d.max_det; k += blockDim.x) {
-    keep_rows[(size_t)img * d.max_det + k] = -1;
-    float* o = dets + ((size_t)img * d.max_det + k) * 7;
-    for (int t = 0; t < 7; ++t) o[t] = 0.0f;
-  }
-}
-
 }  // namespace
 
 extern "C" ycx_status ycx_decode(const ycx_decode_desc* d, const float* head, float* out, void* stream) {
@@ -352,24 +210,5 @@ extern "C" ycx_status ycx_decode_filter(const ycx_decode_filter_desc* d, const f
   dim3 grid(ycx_cdiv(d->rows_total, 256), d->n);
   hipLaunchKernelGGL(decode_filter_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a, cand,
                      cand_rows, cand_counts);
-  return ycx_launch_status();
-}
-
-extern "C" size_t ycx_nms_workspace_size(const ycx_nms_desc* d) {
-  if (!d || d->n <= 0 || d->rows_total <= 0) return 0;
-  return nms_layout(d->rows_total).per_image * (size_t)d->n;
-}
-
-extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, const int32_t* cand_rows,
-                                   const int32_t* cand_counts, void* workspace, size_t workspace_bytes, float* dets,
-                                   int32_t* keep_rows, int32_t* keep_counts, void* stream) {
-  YCX_CHECK_ARG(d && cand && cand_rows && cand_counts && workspace && dets && keep_rows && keep_counts);
-  YCX_CHECK_ARG(d->n > 0 && d->rows_total > 0 && d->nc > 0 && d->max_det > 0);
-  if (workspace_bytes < ycx_nms_workspace_size(d)) return YCX_ERR_CAPACITY;
-  const int rb = row_bits(d->rows_total);
-  YCX_CHECK_SUPPORTED(rb <= 17 && d->rows_total <= kLdsKeys * 16);
-  YCX_CHECK_SUPPORTED((long long)d->nc <= (1LL << (32 - rb)));
-  hipLaunchKernelGGL(sort_nms_kernel, dim3(d->n), dim3(kNmsThreads), 0, reinterpret_cast<hipStream_t>(stream), *d,
-                     cand, cand_rows, cand_counts, (char*)workspace, dets, keep_rows, keep_counts);
   return ycx_launch_status();
 }
