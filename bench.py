@@ -64,11 +64,13 @@ def roofline(det, steps, precision):
     for e in evs:  # materialise the underlying hipEvent_t
         e.record()
     per = {}
+    per_op = [0.0] * n
     for _ in range(steps):
         eng.run_static(events=evs)
         torch.cuda.synchronize()
         for i, info in enumerate(eng.op_info):
             ms = evs[i].elapsed_time(evs[i + 1])
+            per_op[i] += ms / steps
             d = per.setdefault(info['name'], dict(ms=0.0, launches=0, flops=0))
             d['ms'] += ms
             d['launches'] += 1
@@ -86,7 +88,10 @@ def roofline(det, steps, precision):
     all_conv_ms = sum(v['ms'] for v in per.values() if v['flops'] > 0)
     all_conv_tf = sum(v['flops'] for v in per.values()) / (all_conv_ms * 1e-3) / 1e12
     fwd_ms = sum(v['ms'] for v in per.values())
-    return dict(kernel=dom, avg_launch_ms=avg_ms, flops_per_launch=flops_per_launch, achieved=achieved,
+    ops = [dict(i=i, name=info['name'], ms=round(per_op[i], 5), shape=info.get('shape'),
+                tflops=round(info['flops'] / (per_op[i] * 1e-3) / 1e12, 1) if info.get('flops') else None)
+           for i, info in enumerate(eng.op_info)]
+    return dict(kernel=dom, avg_launch_ms=avg_ms, ops=ops, flops_per_launch=flops_per_launch, achieved=achieved,
                 all_conv_tflops=all_conv_tf, all_conv_ms=all_conv_ms, forward_kernel_ms=fwd_ms,
                 per_kernel={k: dict(ms=round(v['ms'], 4), launches=v['launches'],
                                     tflops=(round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1) if v['flops'] else None))
@@ -218,7 +223,7 @@ def main():
         print(json.dumps(out), flush=True)
         if os.environ.get("YCX_BENCH_KERNELS"):
             with open(os.environ["YCX_BENCH_KERNELS"], "w") as f:
-                json.dump(rl['per_kernel'], f, indent=1)
+                json.dump(dict(per_kernel=rl['per_kernel'], ops=rl['ops']), f, indent=1)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -70,7 +70,8 @@ def _run_conv(device, n, h, w, cin, cout, k, s, act, tile, dtype, in_extra=0, ou
     return got, ref
 
 
-TILES_BF16 = [(1, 128, 64), (2, 64, 64), (3, 64, 64), (4, 128, 64), (5, 32, 32), (6, 64, 32), (7, 128, 32)]
+TILES_BF16 = [(1, 128, 64), (2, 64, 64), (3, 64, 64), (4, 128, 64), (5, 32, 32), (6, 64, 32), (7, 128, 32),
+              (9, 128, 64), (10, 64, 64), (11, 256, 128), (12, 128, 64)]
 
 
 @pytest.mark.parametrize('tile,cout,cin', TILES_BF16)

@@ -22,6 +22,7 @@
 // f32 path ("parity mode"): same structure on v_mfma_f32_16x16x4_f32 (exact
 // fp32 FMA chain), used to prove the 1e-3 relative bound vs the fp32 CPU
 // reference.
+#include <algorithm>
 #include "ycx_internal.h"
 
 namespace {
@@ -268,6 +269,179 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
 }
 
 // -------------------------------------------------------------------------
+// bf16 MFMA kernel v2: 512 threads (8 waves), BK = 64, 3-stage LDS-DMA
+// pipeline. Tiles are filled by global_load_lds_dwordx4 (no VGPR staging, no
+// ds_write): each wave-instruction writes 1 KiB = 8 rows x 128 B linearly, so
+// the XOR swizzle of the LDS image is applied on the per-lane SOURCE address
+// (lane -> physical chunk p, fetches logical chunk p ^ swz(row)) and again on
+// the fragment read (guide rule 21). Out-of-image taps and tail rows fetch a
+// zero page instead of being masked. Two stages stay in flight: each K step
+// waits with a counted vmcnt (never 0 inside the loop) and a raw s_barrier.
+// -------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void;
+
+// 16-byte LDS-DMA through a raw buffer descriptor built from uniform values.
+__device__ __forceinline__ void buf_lds16(const void* base, int nbytes, int voff, int soff, void* lds) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nbytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, soff, 0, 0);
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
+  static_assert(WM * WN == 8, "8 waves");
+  constexpr int BK = 64, NST = 3;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_PW = BM / 64, B_PW = BN / 64;  // wave-instructions (8 rows each) per wave per stage
+  constexpr int LPS = A_PW + B_PW;                 // vmcnt per stage per wave
+  constexpr int CP = BM + 4;
+  constexpr int C_BYTES = BN * CP * 4;
+  constexpr int LDS_BYTES = NST * STAGE > C_BYTES ? NST * STAGE : C_BYTES;
+  static_assert(A_PW >= 1 && B_PW >= 1, "tile rows must be multiples of 64");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+
+  const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
+  const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
+  const int ct = L % a.n_ct, pt = L / a.n_ct;
+  const int co0 = ct * BM, px0 = pt * BN;
+  const int lrow = lane >> 3, pch = lane & 7;  // row within the 8-row wave slab, physical chunk
+
+  // Buffer descriptors (raw, stride 0): 32-bit byte offsets, and an offset past
+  // num_records makes the LDS-DMA write zeros (measured on gfx950) — the
+  // padding taps and the pixel tail cost no branch and no zero page.
+  const int w_bytes = a.Cout_pad * a.Ktot * 2, x_bytes = a.N * a.H * a.W * a.in_cs * 2;
+  int a_off[A_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int row = 8 * (wid + 8 * i) + lrow;
+    a_off[i] = ((co0 + row) * a.Ktot + ((pch ^ swz<BK>(row)) << 3)) * 2;
+  }
+  int b_iy0[B_PW], b_ix0[B_PW], b_base[B_PW];
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int row = 8 * (wid + 8 * i) + lrow;
+    const int p = px0 + row;
+    const bool ok = p < a.M;
+    const int pp = ok ? p : 0;
+    const int n = pp / a.HoWo, rem = pp - n * a.HoWo;
+    const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    b_iy0[i] = ok ? oy * a.S - a.P : -(1 << 20);  // tail rows fail the bounds test
+    b_ix0[i] = ox * a.S - a.P;
+    b_base[i] = (((n * a.H + b_iy0[i]) * a.W + b_ix0[i]) * a.in_cs + a.in_coff + ((pch ^ swz<BK>(row)) << 3)) * 2;
+  }
+
+  int i_ky = 0, i_kx = 0, i_cb = 0;  // K position of the next stage to issue
+  auto issue = [&](int s, int buf) {
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * (BK * 2), base + (wid + 8 * i) * 1024);
+    const int tap = ((i_ky * a.W + i_kx) * a.in_cs + i_cb) * 2;  // uniform
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      const bool ok = (unsigned)(b_iy0[i] + i_ky) < (unsigned)a.H && (unsigned)(b_ix0[i] + i_kx) < (unsigned)a.W;
+      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + A_BYTES + (wid + 8 * i) * 1024);
+    }
+    i_cb += BK;
+    if (i_cb == a.Cin) {
+      i_cb = 0;
+      if (++i_kx == a.KW) { i_kx = 0; ++i_ky; }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = a.nsteps;
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 2 < nt) issue(t + 2, (t + 2) % NST);
+    const __bf16* A = reinterpret_cast<const __bf16*>(smem + (t % NST) * STAGE);
+    const __bf16* B = reinterpret_cast<const __bf16*>(smem + (t % NST) * STAGE + A_BYTES);
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int c = kk * 4 + (lane >> 4);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * TM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(A + row * BK + ((c ^ swz<BK>(row)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * TN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(B + row * BK + ((c ^ swz<BK>(row)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // Epilogue (as v1): bias + act into an fp32 LDS tile, then 16-B coalesced stores.
+  if (a.out_layout == YCX_OUT_NCHW_F32) {
+    float* Y = reinterpret_cast<float*>(a.y);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        int p = px0 + wn * TN + j * 16 + (lane & 15);
+        if (p >= a.M) continue;
+        int n = p / a.HoWo, rem = p - n * a.HoWo;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int co = co0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          if (co < a.Cout)
+            Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] =
+                ycx_act<true>(acc[i][j][r] + a.bias[co], a.act, a.slope);
+        }
+      }
+    return;
+  }
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int col = wm * TM + i * 16 + (lane >> 4) * 4;
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.bias + co0 + col);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * TN + j * 16 + (lane & 15);
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = ycx_act<true>(acc[i][j][r] + bv[r], a.act, a.slope);
+      *reinterpret_cast<f32x4*>(Cs + row * CP + col) = v;
+    }
+  }
+  __syncthreads();
+  constexpr int CCH = BM / 8;
+  for (int idx = tid; idx < BN * CCH; idx += 512) {
+    const int row = idx / CCH, c8 = idx - row * CCH;
+    const int p = px0 + row, co = co0 + c8 * 8;
+    if (p >= a.M || co >= a.Cout) continue;
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * CP + c8 * 8);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * CP + c8 * 8 + 4);
+    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    store8<__bf16>(a, p, co, v);
+  }
+}
+
+// -------------------------------------------------------------------------
 // fp32 parity kernel: 64x64 tile, BK=16, v_mfma_f32_16x16x4_f32.
 // -------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) conv_f32_kernel(ConvArgs a) {
@@ -396,8 +570,9 @@ __global__ void __launch_bounds__(256) stem_kernel(ConvArgs a) {
   for (int i = threadIdx.x; i < wn; i += blockDim.x) ws[i] = Wt[i];
   for (int i = threadIdx.x; i < a.Cout_pad; i += blockDim.x) ws[wn + i] = a.bias[i];
   __syncthreads();
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= a.M) return;
+  const int pr = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool pv = pr < a.M;  // tail threads compute a duplicate pixel and store nothing
+  const int p = pv ? pr : a.M - 1;
   const int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
   const float* X = reinterpret_cast<const float*>(a.x);
   float patch[NT];
@@ -428,7 +603,83 @@ __global__ void __launch_bounds__(256) stem_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = ycx_act<sizeof(OutT) == 2>(v[j] + ws[wn + c0 + j], a.act, a.slope);
-    store8<OutT>(a, p, c0, v);
+    if (pv) store8<OutT>(a, p, c0, v);
+  }
+}
+
+// -------------------------------------------------------------------------
+// MFMA stem (bf16): K = KH*KW*CIN <= 32 is ONE v_mfma_f32_16x16x32_bf16 step.
+// A = folded weights [co][k] held in registers for the whole kernel (lane l:
+// co = 16t + (l&15), k = 8(l>>4) + j); B = im2col gathered straight from the
+// fp32 NCHW image (lane l: pixel l&15 of a 16-pixel group, the same 8 k),
+// converted to bf16 in registers. Each wave grid-strides over 16-pixel groups;
+// the 16 x Cout output tile goes through a per-wave LDS transpose so the
+// store is one contiguous 16 x Cout*2 byte run.
+// -------------------------------------------------------------------------
+template <int KH, int KW, int CIN, int CT>
+__global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
+  constexpr int KT = KH * KW * CIN, COUT = CT * 16;
+  static_assert(KT <= 32, "one MFMA K step");
+  __shared__ __attribute__((aligned(16))) __bf16 stage[4][16 * COUT];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float* Wt = reinterpret_cast<const float*>(a.w);  // [KT][Cout_pad]
+  const float* X = reinterpret_cast<const float*>(a.x);
+  bf16x8 af[CT];
+  int dy[8], dx[8], dc[8];
+  bool kv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * (lane >> 4) + j;
+    kv[j] = k < KT;
+    const int kk = kv[j] ? k : 0, tap = kk / CIN;
+    dc[j] = kk - tap * CIN;
+    dy[j] = tap / KW;
+    dx[j] = tap - dy[j] * KW;
+#pragma unroll
+    for (int t = 0; t < CT; ++t) af[t][j] = (__bf16)(kv[j] ? Wt[kk * a.Cout_pad + t * 16 + (lane & 15)] : 0.0f);
+  }
+  float bias[CT][4];
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[t][r] = a.bias[t * 16 + (lane >> 4) * 4 + r];
+  const int ngroups = (a.M + 15) / 16;
+  const int gstride = gridDim.x * 4;
+  __bf16* st = stage[wv];
+  char* Y = reinterpret_cast<char*>(a.y);
+  for (int g = blockIdx.x * 4 + wv; g < ngroups; g += gstride) {
+    const int pr = g * 16 + (lane & 15);
+    const int p = pr < a.M ? pr : a.M - 1;
+    const int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    bf16x8 bfr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int iy = oy * a.S - a.P + dy[j], ix = ox * a.S - a.P + dx[j];
+      const bool ok = kv[j] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      bfr[j] = (__bf16)(ok ? X[(((size_t)n * a.in_cs + a.in_coff + dc[j]) * a.H + iy) * a.W + ix] : 0.0f);
+    }
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (__bf16)ycx_act<true>(acc[r] + bias[t][r], a.act, a.slope);
+      // D[co][px]: px = lane & 15, co = 16t + 4(lane>>4) + r
+      *reinterpret_cast<bf16x4*>(st + (lane & 15) * COUT + t * 16 + (lane >> 4) * 4) = o;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int CPP = COUT * 2 / 16;  // 16-byte chunks per pixel
+#pragma unroll
+    for (int c = lane; c < 16 * CPP; c += 64) {
+      const int px = c / CPP, ch = c - px * CPP;
+      if (g * 16 + px < a.M && ch * 8 < a.Cout)
+        *reinterpret_cast<bf16x8*>(Y + ((size_t)(g * 16 + px) * a.out_cs + a.out_coff) * 2 + ch * 16) =
+            *reinterpret_cast<const bf16x8*>(st + px * COUT + ch * 8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -462,6 +713,10 @@ const TileInfo kTiles[] = {
     {64, 256, 32, "bf16_co64_px256_k32"},
     {128, 128, 32, "bf16_co128_px128_k32"},
     {64, 64, 16, "f32_co64_px64_k16"},
+    {128, 256, 64, "glds_co128_px256_k64"},
+    {64, 256, 64, "glds_co64_px256_k64"},
+    {256, 128, 64, "glds_co256_px128_k64"},
+    {128, 128, 64, "glds_co128_px128_k64"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -472,6 +727,15 @@ ycx_status launch_bf16(ConvArgs a, hipStream_t st) {
   int n_pt = (a.M + BN - 1) / BN;
   a.nwg = a.n_ct * n_pt;
   hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, BK, WM, WN>), dim3(a.nwg), dim3(256), 0, st, a);
+  return ycx_launch_status();
+}
+
+template <int BM, int BN, int WM, int WN>
+ycx_status launch_glds(ConvArgs a, hipStream_t st) {
+  a.nsteps = a.KH * a.KW * (a.Cin / 64);
+  a.n_ct = a.Cout_pad / BM;
+  a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
+  hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN>), dim3(a.nwg), dim3(512), 0, st, a);
   return ycx_launch_status();
 }
 
@@ -495,12 +759,18 @@ extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {
     if (d->cout_pad % 64 == 0) return 6;
     return 5;
   }
+  // 512-thread LDS-DMA kernels (one workgroup per CU) where they fill the chip;
+  // their buffer descriptors address < 2 GiB per operand.
+  const bool fits = (long long)d->n * d->h * d->w * d->in_c_stride * 2 < (1LL << 31) &&
+                    (long long)d->cout_pad * d->kh * d->kw * d->cin * 2 < (1LL << 31);
+  if (!fits) return d->cout_pad % 128 == 0 ? 1 : 2;
   if (d->cout_pad % 128 == 0) {
-    long long blocks = (d->cout_pad / 128) * ((M + 127) / 128);
-    if (blocks >= 512) return 1;
-    return 4;  // co128 x px64: twice the blocks for small-M (deep) layers
+    if ((d->cout_pad / 128) * ((M + 255) / 256) >= 256) return 9;
+    if ((d->cout_pad / 128) * ((M + 127) / 128) >= 256) return 12;
+    return 4;  // co128 x px64, 256 threads: more blocks for small-M (deep) layers
   }
   if (d->cout_pad % 64 == 0) {
+    if ((M + 255) / 256 >= 256) return 10;
     long long blocks = (d->cout_pad / 64) * ((M + 255) / 256);
     if (blocks >= 512) return 2;
     return 3;
@@ -553,6 +823,10 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
     case 5: return launch_bf16<32, 256, 32, 1, 4>(a, st);
     case 6: return launch_bf16<64, 256, 32, 1, 4>(a, st);
     case 7: return launch_bf16<128, 128, 32, 2, 2>(a, st);
+    case 9: return launch_glds<128, 256, 2, 4>(a, st);
+    case 10: return launch_glds<64, 256, 1, 8>(a, st);
+    case 11: return launch_glds<256, 128, 4, 2>(a, st);
+    case 12: return launch_glds<128, 128, 2, 4>(a, st);
     default: return YCX_ERR_UNSUPPORTED;
   }
 }
@@ -571,10 +845,27 @@ extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, cons
   YCX_CHECK_SUPPORTED((long long)d->n * d->ho * d->wo < (1LL << 31));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ConvArgs a = make_args(d, x, w, bias, y, nullptr);
+  const bool bf = d->dtype == YCX_DT_BF16;
+  if (bf && d->out_layout == YCX_OUT_NHWC && (d->cout_pad == 32 || d->cout_pad == 64)) {
+    const long long groups = ((long long)a.M + 15) / 16;
+    dim3 g((unsigned)std::min<long long>((groups + 3) / 4, 256LL * 16));
+#define YCX_STEM_MFMA(KH_, KW_, CI_)                                                           \
+    if (d->kh == KH_ && d->kw == KW_ && d->cin == CI_) {                                       \
+      if (d->cout_pad == 32)                                                                   \
+        hipLaunchKernelGGL((stem_mfma<KH_, KW_, CI_, 2>), g, dim3(256), 0, st, a);             \
+      else                                                                                     \
+        hipLaunchKernelGGL((stem_mfma<KH_, KW_, CI_, 4>), g, dim3(256), 0, st, a);             \
+      return ycx_launch_status();                                                              \
+    }
+    YCX_STEM_MFMA(3, 3, 3)
+    YCX_STEM_MFMA(3, 3, 1)
+    YCX_STEM_MFMA(1, 1, 3)
+    YCX_STEM_MFMA(5, 5, 1)
+#undef YCX_STEM_MFMA
+  }
   const size_t lds = ((size_t)d->kh * d->kw * d->cin * d->cout_pad + d->cout_pad) * sizeof(float);
   YCX_CHECK_SUPPORTED(lds <= 64 * 1024);
   dim3 grid(ycx_cdiv(a.M, 256));
-  const bool bf = d->dtype == YCX_DT_BF16;
 #define YCX_STEM(KH_, KW_, CI_)                                                                  \
   if (d->kh == KH_ && d->kw == KW_ && d->cin == CI_) {                                           \
     if (bf)                                                                                      \
