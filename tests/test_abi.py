@@ -47,13 +47,16 @@ def test_tile_picker():
     from ycx import _lib
     d = _lib.ConvDesc()
     d.n, d.ho, d.wo, d.cin, d.cout_pad, d.dtype = 32, 160, 160, 64, 64, _lib.DT_BF16
-    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 10   # 512-thread LDS-DMA co64 x px256
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 15   # 512-thread 2-stage LDS-DMA co64 x px256
     d.cin = 32
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 17  # two taps per K step
+    d.ho = d.wo = 20
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 6
+    d.ho = d.wo = 160
     d.cout_pad = 32
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 5
     d.cin, d.cout_pad, d.ho, d.wo = 512, 512, 20, 20
-    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) in (4, 9, 12)
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 16
     d.dtype = _lib.DT_F32
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 8
 

@@ -71,11 +71,12 @@ def _run_conv(device, n, h, w, cin, cout, k, s, act, tile, dtype, in_extra=0, ou
 
 
 TILES_BF16 = [(1, 128, 64), (2, 64, 64), (3, 64, 64), (4, 128, 64), (5, 32, 32), (6, 64, 32), (7, 128, 32),
-              (9, 128, 64), (10, 64, 64), (11, 256, 128), (12, 128, 64)]
+              (9, 128, 64), (10, 64, 64), (11, 256, 128), (12, 128, 64), (13, 64, 32), (14, 128, 32), (14, 256, 32),
+              (15, 64, 64), (16, 128, 64), (17, 64, 32), (18, 64, 128)]
 
 
 @pytest.mark.parametrize('tile,cout,cin', TILES_BF16)
-@pytest.mark.parametrize('k,s', [(3, 1), (1, 1), (3, 2)])
+@pytest.mark.parametrize('k,s', [(3, 1), (1, 1), (3, 2), (5, 1)])
 def test_conv_bf16_tiles(device, tile, cout, cin, k, s):
     got, ref = _run_conv(device, 2, 13, 11, cin, cout, k, s, L.ACT_SILU, tile, L.DT_BF16, in_extra=8, out_extra=16)
     # bf16 output rounding (2^-8 relative) on top of exact products of bf16 inputs
@@ -158,8 +159,9 @@ def test_copy_upsample(device, dtype, scale, nchw):
 
 @pytest.mark.parametrize('cin,k,s', [(3, 3, 1), (3, 3, 2), (1, 3, 1)])
 @pytest.mark.parametrize('dtype', [L.DT_BF16, L.DT_F32])
-def test_stem(device, cin, k, s, dtype):
-    n, h, w, cout = 2, 17, 19, 32
+@pytest.mark.parametrize('h,w,cout', [(17, 19, 32), (18, 32, 32), (9, 64, 64)])  # wo % 16 == 0: MFMA stem
+def test_stem(device, cin, k, s, dtype, h, w, cout):
+    n = 2
     x = torch.rand(n, cin, h, w)
     wt = torch.randn(cout, cin, k, k) * 0.3
     b = torch.randn(cout) * 0.1

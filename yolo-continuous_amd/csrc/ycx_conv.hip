@@ -88,6 +88,33 @@ __device__ __forceinline__ void store8(const ConvArgs& a, int p, int co, float v
   }
 }
 
+// Writes 4 consecutive bf16 output channels of pixel p straight from an MFMA
+// accumulator (8-byte store; the 4 lane groups of a 16x16 tile complete 32
+// contiguous bytes per pixel and L2 merges the lines), residual added first.
+__device__ __forceinline__ void store4_bf16(const ConvArgs& a, int p, int co, float v[4]) {
+  if (a.res) {
+    const bf16x4 rv = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.res) +
+                                                       (size_t)p * a.res_cs + a.res_coff + co);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += (float)rv[j];
+  }
+  bf16x4 ov;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ov[j] = (__bf16)v[j];
+  __bf16* base = reinterpret_cast<__bf16*>(a.y) + a.out_coff + co;
+  if (a.out_layout == YCX_OUT_NHWC_UP2) {
+    const int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    const size_t W2 = 2 * (size_t)a.Wo;
+    const size_t b0 = ((size_t)n * 2 * a.Ho + 2 * oy) * W2 + 2 * ox;
+    *reinterpret_cast<bf16x4*>(base + b0 * a.out_cs) = ov;
+    *reinterpret_cast<bf16x4*>(base + (b0 + 1) * a.out_cs) = ov;
+    *reinterpret_cast<bf16x4*>(base + (b0 + W2) * a.out_cs) = ov;
+    *reinterpret_cast<bf16x4*>(base + (b0 + W2 + 1) * a.out_cs) = ov;
+  } else {
+    *reinterpret_cast<bf16x4*>(base + (size_t)p * a.out_cs) = ov;
+  }
+}
+
 // -------------------------------------------------------------------------
 // bf16 MFMA kernel
 // -------------------------------------------------------------------------
@@ -286,18 +313,24 @@ __device__ __forceinline__ void buf_lds16(const void* base, int nbytes, int voff
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, soff, 0, 0);
 }
 
-template <int BM, int BN, int WM, int WN>
+// TT (two taps per K step) serves Cin == 32: one 64-wide K step spans taps
+// 2s and 2s+1, and each lane's logical chunk c = pch ^ swz(row) (constant per
+// lane across steps) selects tap 2s + (c >> 2) and channels 8(c & 3). The
+// weights stay linear in k, so only the activation side changes; an odd last
+// tap fetches zeros on the activation side (its weight chunk is finite).
+// NST = 2 halves the LDS so two workgroups share a CU: one block's prologue
+// and epilogue then overlap the other's MFMA loop (short-K layers).
+template <int BM, int BN, int WM, int WN, bool TT, int NST>
 __global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
   static_assert(WM * WN == 8, "8 waves");
-  constexpr int BK = 64, NST = 3;
+  static_assert(NST == 2 || NST == 3, "pipeline depth");
+  constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int A_PW = BM / 64, B_PW = BN / 64;  // wave-instructions (8 rows each) per wave per stage
   constexpr int LPS = A_PW + B_PW;                 // vmcnt per stage per wave
-  constexpr int CP = BM + 4;
-  constexpr int C_BYTES = BN * CP * 4;
-  constexpr int LDS_BYTES = NST * STAGE > C_BYTES ? NST * STAGE : C_BYTES;
+  constexpr int LDS_BYTES = NST * STAGE;           // the epilogue stores straight from registers
   static_assert(A_PW >= 1 && B_PW >= 1, "tile rows must be multiples of 64");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
@@ -331,24 +364,44 @@ __global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
     const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
     b_iy0[i] = ok ? oy * a.S - a.P : -(1 << 20);  // tail rows fail the bounds test
     b_ix0[i] = ox * a.S - a.P;
-    b_base[i] = (((n * a.H + b_iy0[i]) * a.W + b_ix0[i]) * a.in_cs + a.in_coff + ((pch ^ swz<BK>(row)) << 3)) * 2;
+    const int lch = pch ^ swz<BK>(row);  // logical chunk this lane fetches
+    b_base[i] = (((n * a.H + b_iy0[i]) * a.W + b_ix0[i]) * a.in_cs + a.in_coff + ((TT ? lch & 3 : lch) << 3)) * 2;
   }
+  // swz<64>(row) = (4 wid + lrow / 2) & 7 for every i: one tap select per lane.
+  const bool sel1 = TT && ((pch ^ swz<BK>(8 * wid + lrow)) >> 2);
 
-  int i_ky = 0, i_kx = 0, i_cb = 0;  // K position of the next stage to issue
+  int i_ky = 0, i_kx = 0, i_cb = 0;  // K position (first tap) of the next stage to issue
+  const int ntaps = a.KH * a.KW;
+  int i_tap = 0;
   auto issue = [&](int s, int buf) {
     char* base = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * (BK * 2), base + (wid + 8 * i) * 1024);
-    const int tap = ((i_ky * a.W + i_kx) * a.in_cs + i_cb) * 2;  // uniform
+    int ky = i_ky, kx = i_kx;
+    if (TT) {
+      // second tap of the pair; past the last tap it can never pass the bounds test
+      int ky1 = i_ky, kx1 = i_kx + 1;
+      if (kx1 == a.KW) { kx1 = 0; ++ky1; }
+      if (i_tap + 1 >= ntaps) ky1 = -(1 << 22);
+      ky = sel1 ? ky1 : ky;
+      kx = sel1 ? kx1 : kx;
+    }
+    const int tap = ((ky * a.W + kx) * a.in_cs + i_cb) * 2;
 #pragma unroll
     for (int i = 0; i < B_PW; ++i) {
-      const bool ok = (unsigned)(b_iy0[i] + i_ky) < (unsigned)a.H && (unsigned)(b_ix0[i] + i_kx) < (unsigned)a.W;
+      const bool ok = (unsigned)(b_iy0[i] + ky) < (unsigned)a.H && (unsigned)(b_ix0[i] + kx) < (unsigned)a.W;
       buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + A_BYTES + (wid + 8 * i) * 1024);
     }
-    i_cb += BK;
-    if (i_cb == a.Cin) {
-      i_cb = 0;
-      if (++i_kx == a.KW) { i_kx = 0; ++i_ky; }
+    if (TT) {
+      i_tap += 2;
+      i_kx += 2;
+      while (i_kx >= a.KW) { i_kx -= a.KW; ++i_ky; }
+    } else {
+      i_cb += BK;
+      if (i_cb == a.Cin) {
+        i_cb = 0;
+        if (++i_kx == a.KW) { i_kx = 0; ++i_ky; }
+      }
     }
   };
 
@@ -360,13 +413,13 @@ __global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
 
   const int nt = a.nsteps;
   issue(0, 0);
-  if (nt > 1) issue(1, 1);
+  if (NST == 3 && nt > 1) issue(1, 1);
   for (int t = 0; t < nt; ++t) {
-    if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+    if (NST == 3 && t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 2 < nt) issue(t + 2, (t + 2) % NST);
+    if (t + NST - 1 < nt) issue(t + NST - 1, (t + NST - 1) % NST);
     const __bf16* A = reinterpret_cast<const __bf16*>(smem + (t % NST) * STAGE);
     const __bf16* B = reinterpret_cast<const __bf16*>(smem + (t % NST) * STAGE + A_BYTES);
 #pragma unroll
@@ -391,10 +444,7 @@ __global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // Epilogue (as v1): bias + act into an fp32 LDS tile, then 16-B coalesced stores.
+  // Epilogue: bias + act (+ residual) straight from the accumulators.
   if (a.out_layout == YCX_OUT_NCHW_F32) {
     float* Y = reinterpret_cast<float*>(a.y);
 #pragma unroll
@@ -414,30 +464,20 @@ __global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
       }
     return;
   }
-  float* Cs = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int col = wm * TM + i * 16 + (lane >> 4) * 4;
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.bias + co0 + col);
+    const int co = co0 + wm * TM + i * 16 + (lane >> 4) * 4;
+    if (co >= a.Cout) continue;  // cout % 8 == 0, co % 4 == 0: the 4 channels are all valid
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.bias + co);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int row = wn * TN + j * 16 + (lane & 15);
-      f32x4 v;
+      const int p = px0 + wn * TN + j * 16 + (lane & 15);
+      if (p >= a.M) continue;
+      float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = ycx_act<true>(acc[i][j][r] + bv[r], a.act, a.slope);
-      *reinterpret_cast<f32x4*>(Cs + row * CP + col) = v;
+      store4_bf16(a, p, co, v);
     }
-  }
-  __syncthreads();
-  constexpr int CCH = BM / 8;
-  for (int idx = tid; idx < BN * CCH; idx += 512) {
-    const int row = idx / CCH, c8 = idx - row * CCH;
-    const int p = px0 + row, co = co0 + c8 * 8;
-    if (p >= a.M || co >= a.Cout) continue;
-    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * CP + c8 * 8);
-    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * CP + c8 * 8 + 4);
-    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    store8<__bf16>(a, p, co, v);
   }
 }
 
@@ -609,77 +649,77 @@ __global__ void __launch_bounds__(256) stem_kernel(ConvArgs a) {
 
 // -------------------------------------------------------------------------
 // MFMA stem (bf16): K = KH*KW*CIN <= 32 is ONE v_mfma_f32_16x16x32_bf16 step.
-// A = folded weights [co][k] held in registers for the whole kernel (lane l:
-// co = 16t + (l&15), k = 8(l>>4) + j); B = im2col gathered straight from the
-// fp32 NCHW image (lane l: pixel l&15 of a 16-pixel group, the same 8 k),
-// converted to bf16 in registers. Each wave grid-strides over 16-pixel groups;
-// the 16 x Cout output tile goes through a per-wave LDS transpose so the
-// store is one contiguous 16 x Cout*2 byte run.
+// A = folded weights held in registers for the whole kernel; B = im2col
+// gathered straight from the fp32 NCHW image (lane l: pixel l&15 of a
+// 16-pixel run, k = 8(l>>4) + j), converted to bf16 in registers. A wave
+// owns whole 16-pixel runs of one output row (Wo % 16 == 0), so the pixel ->
+// (n, oy, ox) split is scalar and each gather is one add from a per-lane tap
+// offset. A-rows are permuted so that the two MFMAs of a pair leave 8
+// consecutive channels in each lane: one 16-byte store per lane, a wave
+// writes 16 pixels x 32 channels as one contiguous KiB.
 // -------------------------------------------------------------------------
+__device__ __forceinline__ int stem_ch(int t, int m) {  // MFMA t, A-row m -> output channel
+  return 32 * (t >> 1) + 8 * (m >> 2) + 4 * (t & 1) + (m & 3);
+}
+
 template <int KH, int KW, int CIN, int CT>
 __global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
-  constexpr int KT = KH * KW * CIN, COUT = CT * 16;
-  static_assert(KT <= 32, "one MFMA K step");
-  __shared__ __attribute__((aligned(16))) __bf16 stage[4][16 * COUT];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int KT = KH * KW * CIN;
+  static_assert(KT <= 32 && CT % 2 == 0, "one MFMA K step, channel pairs");
+  const int lane = threadIdx.x & 63, lx = lane & 15, kq = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const float* Wt = reinterpret_cast<const float*>(a.w);  // [KT][Cout_pad]
-  const float* X = reinterpret_cast<const float*>(a.x);
+  const float* __restrict__ X = reinterpret_cast<const float*>(a.x);
+  const int HW = a.H * a.W;
   bf16x8 af[CT];
-  int dy[8], dx[8], dc[8];
+  int dy[8], dx[8], toff[8];
   bool kv[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int k = 8 * (lane >> 4) + j;
+    const int k = 8 * kq + j;
     kv[j] = k < KT;
-    const int kk = kv[j] ? k : 0, tap = kk / CIN;
-    dc[j] = kk - tap * CIN;
+    const int kk = kv[j] ? k : 0, tap = kk / CIN, dc = kk - tap * CIN;
     dy[j] = tap / KW;
     dx[j] = tap - dy[j] * KW;
+    toff[j] = dc * HW + dy[j] * a.W + dx[j];
 #pragma unroll
-    for (int t = 0; t < CT; ++t) af[t][j] = (__bf16)(kv[j] ? Wt[kk * a.Cout_pad + t * 16 + (lane & 15)] : 0.0f);
+    for (int t = 0; t < CT; ++t) af[t][j] = (__bf16)(kv[j] ? Wt[kk * a.Cout_pad + stem_ch(t, lx)] : 0.0f);
   }
   float bias[CT][4];
 #pragma unroll
   for (int t = 0; t < CT; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bias[t][r] = a.bias[t * 16 + (lane >> 4) * 4 + r];
-  const int ngroups = (a.M + 15) / 16;
-  const int gstride = gridDim.x * 4;
-  __bf16* st = stage[wv];
-  char* Y = reinterpret_cast<char*>(a.y);
-  for (int g = blockIdx.x * 4 + wv; g < ngroups; g += gstride) {
-    const int pr = g * 16 + (lane & 15);
-    const int p = pr < a.M ? pr : a.M - 1;
-    const int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
-    bf16x8 bfr;
+    for (int r = 0; r < 4; ++r) bias[t][r] = a.bias[stem_ch(t, 4 * kq + r)];
+  const int ngroups = a.M / 16;
+  char* __restrict__ Y = reinterpret_cast<char*>(a.y);
+  for (int g = blockIdx.x * 4 + wv; g < ngroups; g += gridDim.x * 4) {
+    const int p0 = g * 16;  // scalar: the run lies in one output row
+    const int n = p0 / a.HoWo, rem = p0 - n * a.HoWo, oy = rem / a.Wo, ox0 = rem - oy * a.Wo;
+    const float* Xn = X + (size_t)(n * a.in_cs + a.in_coff) * HW;
+    const int iy0 = oy * a.S - a.P, ixl = (ox0 + lx) * a.S - a.P;
+    const int base = iy0 * a.W + ixl;
+    bf16x8 b;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int iy = oy * a.S - a.P + dy[j], ix = ox * a.S - a.P + dx[j];
-      const bool ok = kv[j] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-      bfr[j] = (__bf16)(ok ? X[(((size_t)n * a.in_cs + a.in_coff + dc[j]) * a.H + iy) * a.W + ix] : 0.0f);
+      const bool ok = kv[j] && (unsigned)(iy0 + dy[j]) < (unsigned)a.H && (unsigned)(ixl + dx[j]) < (unsigned)a.W;
+      b[j] = (__bf16)(ok ? Xn[base + toff[j]] : 0.0f);
     }
 #pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      bf16x4 o;
+    for (int q = 0; q < CT / 2; ++q) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2 * q], b, z, 0, 0, 0);
+      const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2 * q + 1], b, z, 0, 0, 0);
+      const int ch0 = 32 * q + 8 * kq;
+      if (ch0 < a.Cout) {
+        bf16x8 o;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (__bf16)ycx_act<true>(acc[r] + bias[t][r], a.act, a.slope);
-      // D[co][px]: px = lane & 15, co = 16t + 4(lane>>4) + r
-      *reinterpret_cast<bf16x4*>(st + (lane & 15) * COUT + t * 16 + (lane >> 4) * 4) = o;
+        for (int r = 0; r < 4; ++r) {
+          o[r] = (__bf16)ycx_act<true>(c0[r] + bias[2 * q][r], a.act, a.slope);
+          o[4 + r] = (__bf16)ycx_act<true>(c1[r] + bias[2 * q + 1][r], a.act, a.slope);
+        }
+        *reinterpret_cast<bf16x8*>(Y + ((size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) * 2) = o;
+      }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    constexpr int CPP = COUT * 2 / 16;  // 16-byte chunks per pixel
-#pragma unroll
-    for (int c = lane; c < 16 * CPP; c += 64) {
-      const int px = c / CPP, ch = c - px * CPP;
-      if (g * 16 + px < a.M && ch * 8 < a.Cout)
-        *reinterpret_cast<bf16x8*>(Y + ((size_t)(g * 16 + px) * a.out_cs + a.out_coff) * 2 + ch * 16) =
-            *reinterpret_cast<const bf16x8*>(st + px * COUT + ch * 8);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -717,6 +757,12 @@ const TileInfo kTiles[] = {
     {64, 256, 64, "glds_co64_px256_k64"},
     {256, 128, 64, "glds_co256_px128_k64"},
     {128, 128, 64, "glds_co128_px128_k64"},
+    {64, 256, 32, "glds2_co64_px256_k32x2"},
+    {128, 256, 32, "glds2_co128_px256_k32x2"},
+    {64, 256, 64, "glds_co64_px256_k64_s2"},
+    {128, 128, 64, "glds_co128_px128_k64_s2"},
+    {64, 256, 32, "glds2_co64_px256_k32x2_s2"},
+    {64, 128, 64, "glds_co64_px128_k64_s2"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -730,12 +776,14 @@ ycx_status launch_bf16(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool TT = false, int NST = 3>
 ycx_status launch_glds(ConvArgs a, hipStream_t st) {
-  a.nsteps = a.KH * a.KW * (a.Cin / 64);
+  if (TT && a.Cin != 32) return YCX_ERR_UNSUPPORTED;
+  if (!TT && a.Cin % 64 != 0) return YCX_ERR_UNSUPPORTED;
+  a.nsteps = TT ? (a.KH * a.KW + 1) / 2 : a.KH * a.KW * (a.Cin / 64);
   a.n_ct = a.Cout_pad / BM;
   a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN>), dim3(a.nwg), dim3(512), 0, st, a);
+  hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST>), dim3(a.nwg), dim3(512), 0, st, a);
   return ycx_launch_status();
 }
 
@@ -754,28 +802,27 @@ extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {
   const long long M = (long long)d->n * d->ho * d->wo;
   const bool k64 = (d->cin % 64) == 0;
   if (d->cout_pad % 64 != 0) return 5;  // cout 32: co32 x px256, BK 32 (cin % 32 == 0)
+  // The 512-thread LDS-DMA kernels' buffer descriptors address < 2 GiB per operand.
+  const bool fits = (long long)d->n * d->h * d->w * d->in_c_stride * 2 < (1LL << 31) &&
+                    (long long)d->cout_pad * d->kh * d->kw * d->cin * 2 < (1LL << 31);
+  // Two-stage LDS-DMA tiles (two workgroups per CU) wherever they fill the chip
+  // (tests/probes/conv_bench.py: 10-40 % over the 3-stage one-per-CU tiles).
+  if (d->cin == 32 && fits) {  // two taps per 64-wide K step
+    if ((d->cout_pad / 64) * ((M + 255) / 256) >= 256) return 17;
+  }
   if (!k64) {
     if (d->cout_pad % 128 == 0 && d->cout_pad >= 128) return 7;
     if (d->cout_pad % 64 == 0) return 6;
     return 5;
   }
-  // 512-thread LDS-DMA kernels (one workgroup per CU) where they fill the chip;
-  // their buffer descriptors address < 2 GiB per operand.
-  const bool fits = (long long)d->n * d->h * d->w * d->in_c_stride * 2 < (1LL << 31) &&
-                    (long long)d->cout_pad * d->kh * d->kw * d->cin * 2 < (1LL << 31);
   if (!fits) return d->cout_pad % 128 == 0 ? 1 : 2;
   if (d->cout_pad % 128 == 0) {
-    if ((d->cout_pad / 128) * ((M + 255) / 256) >= 256) return 9;
-    if ((d->cout_pad / 128) * ((M + 127) / 128) >= 256) return 12;
+    if ((d->cout_pad / 128) * ((M + 127) / 128) >= 256) return 16;
     return 4;  // co128 x px64, 256 threads: more blocks for small-M (deep) layers
   }
-  if (d->cout_pad % 64 == 0) {
-    if ((M + 255) / 256 >= 256) return 10;
-    long long blocks = (d->cout_pad / 64) * ((M + 255) / 256);
-    if (blocks >= 512) return 2;
-    return 3;
-  }
-  return 0;
+  if ((M + 255) / 256 >= 2048) return 15;
+  if ((d->cout_pad / 64) * ((M + 127) / 128) >= 256) return 18;
+  return 3;
 }
 
 extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const void* w, const float* bias,
@@ -827,6 +874,12 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
     case 10: return launch_glds<64, 256, 1, 8>(a, st);
     case 11: return launch_glds<256, 128, 4, 2>(a, st);
     case 12: return launch_glds<128, 128, 2, 4>(a, st);
+    case 13: return launch_glds<64, 256, 1, 8, true>(a, st);
+    case 14: return launch_glds<128, 256, 2, 4, true>(a, st);
+    case 15: return launch_glds<64, 256, 1, 8, false, 2>(a, st);
+    case 16: return launch_glds<128, 128, 2, 4, false, 2>(a, st);
+    case 17: return launch_glds<64, 256, 1, 8, true, 2>(a, st);
+    case 18: return launch_glds<64, 128, 1, 8, false, 2>(a, st);
     default: return YCX_ERR_UNSUPPORTED;
   }
 }
@@ -846,8 +899,8 @@ extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, cons
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ConvArgs a = make_args(d, x, w, bias, y, nullptr);
   const bool bf = d->dtype == YCX_DT_BF16;
-  if (bf && d->out_layout == YCX_OUT_NHWC && (d->cout_pad == 32 || d->cout_pad == 64)) {
-    const long long groups = ((long long)a.M + 15) / 16;
+  if (bf && d->out_layout == YCX_OUT_NHWC && (d->cout_pad == 32 || d->cout_pad == 64) && d->wo % 16 == 0) {
+    const long long groups = (long long)a.M / 16;
     dim3 g((unsigned)std::min<long long>((groups + 3) / 4, 256LL * 16));
 #define YCX_STEM_MFMA(KH_, KW_, CI_)                                                           \
     if (d->kh == KH_ && d->kw == KW_ && d->cin == CI_) {                                       \
