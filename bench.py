@@ -33,9 +33,10 @@ ANCHORS = [[12, 16, 19, 36, 40, 28], [36, 75, 76, 55, 72, 146], [142, 110, 192, 
 MASK = [[6, 7, 8], [3, 4, 5], [0, 1, 2]]
 METRIC = "images/sec (whole node) + p50 end-to-end latency, 640×640 bs=32, 1/2/4/8 MI355X"
 PEAK = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
+ROUND = "r01"  # profiles/<ROUND>/: rocprofv3 summaries of this round's bench command
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -51,7 +52,7 @@ def parse():
     ap.add_argument("--max-det", type=int, default=300)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample (0: skip)")
     ap.add_argument("--roofline-steps", type=int, default=3)
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def roofline(det, steps, precision):
@@ -130,18 +131,10 @@ def cpu_baseline(args, sd, model_cfg, budget_s):
                        f"torch {torch.__version__} CPU, {cores} threads")
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    dev = torch.device(f"cuda:{local}")
-    torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-
+def setup(args, dev, rank=0, use_graph=None):
+    """The bench workload on ``dev``: yolov7 with seeded synthetic weights, a
+    Detector for (batch, 3, size, size) and this rank's synthetic images
+    already resident in HBM."""
     from ycx.detect import Detector
     from ycx.nets.yolo import Model
     from ycx.utils.helper_io import cvt_cfg
@@ -154,18 +147,44 @@ def main():
     model.to(dev)
     shape = (args.batch, 3, args.size, args.size)
     det = Detector(model, shape, dev, ANCHORS, MASK, conf_thres=args.conf, nms_thres=args.iou,
-                   max_det=args.max_det, use_graph=not args.no_graph)
-    # Synthetic images, this rank's shard of the global batch, resident in HBM.
+                   max_det=args.max_det, use_graph=(not args.no_graph) if use_graph is None else use_graph)
     det.x.copy_(synthetic_images(*shape, seed=1000 + rank).to(dev))
+    return model, det, sd, cfg, shape
+
+
+def pmc_traffic(kernel, shape):
+    """HBM bytes per launch of ``kernel`` from this round's PMC passes
+    (tools/pmc_traffic.py -> profiles/<ROUND>/traffic.json), or None."""
+    path = os.path.join(REPO, "profiles", ROUND, "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if list(t.get("shape", [])) != list(shape) or kernel not in t.get("per_name", {}):
+        return None
+    return round(t["per_name"][kernel]["hbm_bytes_per_launch"])
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
     if world > 1:
-        g_dets = torch.empty((world * args.batch, args.max_det, 7), dtype=torch.float32, device=dev)
-        g_cnt = torch.empty((world * args.batch,), dtype=torch.int32, device=dev)
+        dist.init_process_group("nccl", device_id=dev)
+
+    model, det, sd, cfg, shape = setup(args, dev, rank)
+    from ycx.dist import gather_detections
 
     def step():
         dets, keep, kc = det()
-        if world > 1:  # the single collective: all-gather of padded detections (+ counts)
-            dist.all_gather_into_tensor(g_dets, dets)
-            dist.all_gather_into_tensor(g_cnt, kc)
+        if world > 1:  # the single collective: all-gather of padded detections (+ counts, keep rows)
+            dets, kc, keep = gather_detections(dets, kc, keep)
         return kc
 
     for _ in range(args.warmup):
@@ -212,7 +231,8 @@ def main():
             "mfma_fraction_whole_step": round(model.engine_for(shape, dev).flops_per_image * value /
                                               (world * peak * 1e12), 4),
             "roofline": {"bound": "mfma", "kernel": rl['kernel'], "achieved": round(rl['achieved'], 2), "peak": peak,
-                         "unit": "TFLOP/s", "frac": round(rl['achieved'] / peak, 4), "traffic": None,
+                         "unit": "TFLOP/s", "frac": round(rl['achieved'] / peak, 4),
+                         "traffic": pmc_traffic(rl['kernel'], shape), "traffic_unit": "bytes/launch (HBM, PMC)",
                          "avg_launch_ms": round(rl['avg_launch_ms'], 5),
                          "flops_per_launch": int(rl['flops_per_launch']),
                          "all_conv_tflops": round(rl['all_conv_tflops'], 2),

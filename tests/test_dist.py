@@ -1,0 +1,87 @@
+"""N > 1 data-parallel path on CPU: world_size 2 over gloo.
+
+Each rank fabricates its shard's padded detections; after the single
+all-gather every rank must hold all images in rank-major (= original image)
+order, and the host conversion must reproduce the reference's output list
+shape (np.float32 (K, 7) or None per image)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from ycx.dist import gather_detections, shard, to_output_list
+
+MAX_DET = 5
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _fake_shard(images):
+    """Deterministic padded detections for global image ids ``images``."""
+    n = len(images)
+    dets = torch.full((n, MAX_DET, 7), -1.0)
+    keep = torch.full((n, MAX_DET), -1, dtype=torch.int32)
+    cnt = torch.zeros(n, dtype=torch.int32)
+    for i, g in enumerate(images):
+        k = g % (MAX_DET + 1)  # image 0 and 6 keep nothing
+        cnt[i] = k
+        for j in range(k):
+            dets[i, j] = torch.tensor([g, j, g + 1, j + 1, 0.5, 0.25, g % 3], dtype=torch.float32)
+            keep[i, j] = 100 * g + j
+    return dets, keep, cnt
+
+
+def _worker(rank, world, port, global_batch, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sl = shard(global_batch, rank, world)
+        dets, keep, cnt = _fake_shard(list(range(sl.start, sl.stop)))
+        g_dets, g_cnt, g_keep = gather_detections(dets, cnt, keep)
+        q.put((rank, g_dets.numpy(), g_cnt.numpy(), g_keep.numpy()))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_is_a_partition():
+    for gb in (1, 7, 32, 256):
+        for world in (1, 2, 3, 8):
+            ids = [i for r in range(world) for i in range(gb)[shard(gb, r, world)]]
+            assert ids == list(range(gb))
+
+
+@pytest.mark.parametrize("global_batch", [8, 64])
+def test_gather_world2_gloo(global_batch):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, global_batch, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_dets, want_keep, want_cnt = _fake_shard(list(range(global_batch)))
+    for rank, g_dets, g_cnt, g_keep in results:
+        np.testing.assert_array_equal(g_dets, want_dets.numpy())
+        np.testing.assert_array_equal(g_cnt, want_cnt.numpy())
+        np.testing.assert_array_equal(g_keep, want_keep.numpy())
+    out = to_output_list(torch.from_numpy(results[0][1]), torch.from_numpy(results[0][2]))
+    assert len(out) == global_batch
+    for g, o in enumerate(out):
+        k = g % (MAX_DET + 1)
+        if k == 0:
+            assert o is None
+        else:
+            assert o.dtype == np.float32 and o.shape == (k, 7) and o[0, 0] == g
