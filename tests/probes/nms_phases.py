@@ -1,0 +1,52 @@
+"""Per-phase cycle counts of nms_big on the bench workload (development probe).
+
+    make -C yolo-continuous_amd/csrc prof
+    python tests/probes/nms_phases.py
+"""
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["YCX_LIB"] = os.path.join(REPO, "yolo-continuous_amd", "csrc", "build", "libycx_hip_prof.so")
+sys.path[:0] = [REPO, os.path.join(REPO, "yolo-continuous_amd")]
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from ycx import _lib as L  # noqa: E402
+
+PHASES = ["sort", "spatial", "suppressors", "rounds", "compact"]
+
+
+def main():
+    args = bench.parse(["--cpu-seconds", "0"])
+    dev = torch.device("cuda:0")
+    _, det, _, _, _ = bench.setup(args, dev, use_graph=False)
+    det()
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 16)()
+    L.lib.ycx_nms_prof_read(buf, 1)
+    reps = 3
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    det.engine.run_static()
+    e0.record()
+    for _ in range(reps):
+        det.post()
+    e1.record()
+    torch.cuda.synchronize()
+    L.lib.ycx_nms_prof_read(buf, 1)
+    tasks = buf[7] // reps
+    print(f"post ms {e0.elapsed_time(e1) / reps:.3f}  big tasks/step {tasks}")
+    for i, n in enumerate(PHASES):
+        print(f"  {n:12s} {buf[i] / max(1, buf[7]) / 1e3:9.1f} kcycles/task")
+    print(f"  rounds/task {buf[5] / max(1, buf[7]):.1f}   boxes with > kSlots suppressors/task {buf[6] / max(1, buf[7]):.1f}")
+    nt = max(1, buf[7])
+    print(f"  candidate visits/task {buf[8] / nt:.0f}  sum of per-wave max visits x64/task {64 * buf[9] / nt:.0f}  "
+          f"suppressor pairs/task {buf[10] / nt:.0f}")
+    cnt = det.counts.cpu()
+    print("candidates/img", cnt.float().mean().item())
+
+
+if __name__ == "__main__":
+    main()

@@ -143,3 +143,70 @@ def test_detector_graph_matches_eager(device):
     d2, k2, c2 = [t.clone() for t in g.post()]
     torch.cuda.synchronize()
     assert torch.equal(c1, c2) and torch.equal(k1, k2) and torch.equal(d1, d2)
+
+
+def _check_keep(pred, nc, conf, thr):
+    ref_keep, _ = ref_post.nms_keep_rows(pred.clone(), nc, conf, thr)
+    _, keep, kc = nms_device(pred.clone().to('cuda'), nc, conf, thr)
+    keep, kc = keep.cpu().numpy(), kc.cpu().numpy()
+    for b in range(pred.shape[0]):
+        assert int(kc[b]) == len(ref_keep[b]), (b, int(kc[b]), len(ref_keep[b]))
+        np.testing.assert_array_equal(keep[b, :int(kc[b])], ref_keep[b].numpy())
+
+
+def _random_pred(n, rows, nc, seed, scale=1.0, size_lo=-4.0, size_hi=0.0):
+    """Boxes with log-uniform sizes over 10^size_lo..10^size_hi (aspect up to
+    ~10:1) at uniform centres, every row passing the threshold."""
+    g = torch.Generator().manual_seed(seed)
+    pred = torch.zeros(n, rows, 5 + nc)
+    pred[..., 0:2] = torch.rand(n, rows, 2, generator=g) * scale
+    logs = size_lo + (size_hi - size_lo) * torch.rand(n, rows, 2, generator=g)
+    pred[..., 2:4] = (10.0 ** logs) * scale
+    pred[..., 4] = 0.5 + 0.5 * torch.rand(n, rows, generator=g)
+    pred[..., 5:] = torch.rand(n, rows, nc, generator=g)
+    return pred
+
+
+@pytest.mark.parametrize('thr', [0.0, 0.3, 0.65, 1.0])
+def test_nms_spatial_wide_sizes(device, thr):
+    """Large classes (spatial-grid path) with sizes spanning four octaves of
+    ten, down to far below one grid cell: every level/window bound is used."""
+    _check_keep(_random_pred(2, 6000, 2, seed=11), 2, 0.0, thr)
+
+
+def test_nms_spatial_pixel_coords_and_clusters(device):
+    # pixel units (class extent normalisation) and tight clusters of near-duplicates
+    pred = _random_pred(1, 5000, 1, seed=12, scale=640.0, size_lo=-2.5, size_hi=-0.5)
+    g = torch.Generator().manual_seed(13)
+    centers = torch.rand(40, 2, generator=g) * 640
+    idx = torch.randint(0, 40, (2500,), generator=g)
+    pred[0, :2500, 0:2] = centers[idx] + torch.randn(2500, 2, generator=g) * 3.0
+    pred[0, :2500, 2:4] = 40.0 + torch.randn(2500, 2, generator=g) * 4.0
+    _check_keep(pred, 1, 0.0, 0.45)
+
+
+def test_nms_spatial_degenerate_and_identical(device):
+    pred = _random_pred(1, 3000, 1, seed=14, size_lo=-2.0, size_hi=-1.0)
+    pred[0, 0:200, 2] = 0.0                      # zero width
+    pred[0, 200:400, 3] = -0.01                  # negative height (x2 < x1 after conversion)
+    pred[0, 400:420, 0] = float('nan')           # NaN centre
+    pred[0, 420:440, 2] = float('inf')           # infinite width
+    pred[0, 1000:1800, :4] = torch.tensor([0.5, 0.5, 0.1, 0.1])  # 800 identical boxes
+    pred[0, 1000:1800, 4] = 0.9
+    for thr in (0.5, -0.1):                      # negative threshold: every pair compared
+        _check_keep(pred, 1, 0.0, thr)
+
+
+def test_nms_spatial_long_chain(device):
+    """A staircase where each box suppresses only its successor: greedy keeps
+    every other box, and the fixed point needs one round per link."""
+    rows = 1500
+    pred = torch.zeros(1, rows, 6)
+    i = torch.arange(rows, dtype=torch.float32)
+    pred[0, :, 0] = 0.1 + i * 0.0004          # centre steps 0.4 of a box width
+    pred[0, :, 1] = 0.5
+    pred[0, :, 2] = 0.001
+    pred[0, :, 3] = 0.001
+    pred[0, :, 4] = 1.0 - i * 1e-4            # scores descend along the chain
+    pred[0, :, 5] = 1.0
+    _check_keep(pred, 1, 0.0, 0.3)

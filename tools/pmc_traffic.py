@@ -28,8 +28,10 @@ KIB = 1024
 
 
 def _short(name):
+    # names arrive demangled ("(anonymous namespace)::nms_mask(...)") or, when the
+    # demangler gives up on __bf16 template arguments, mangled ("_ZN12_GLOBAL__N_111copy_kernelIDF16b...")
     for k in OURS:
-        if f"::{k}" in name or name.startswith(k):
+        if k in name:
             return k
     return None
 

@@ -2,23 +2,30 @@
 // loop of detect.py:124-137 (unique classes ascending, nms per class, results
 // concatenated class by class) for the whole batch in three launches.
 //
-//  nms_prep    one 1024-thread workgroup per image:
-//              class histogram (LDS atomics) + exclusive scan -> one bucket per
-//              class; every wave pulls whole classes from an LDS counter and a
-//              class of S <= 512 candidates is finished entirely in registers:
-//              64*R keys (score desc, row asc: torchvision's stable descending
-//              sort) bitonic-sorted across lanes (shfl_xor) and register slots,
-//              boxes gathered, greedy suppression with removed/kept flags as
-//              R-bit masks per lane and box i broadcast by readlane — no LDS,
-//              no barrier. Larger classes are bitonic-sorted by the workgroup
-//              (LDS keys up to 8192) and queued as tasks for nms_mask.
-//  nms_mask    the whole GPU: one wave per (large class, 64-row strip) computes
-//              the IoU > thr bitmask of its rows against every later column
-//              (row-major words, j > i only) — the O(S^2) part, fully parallel.
-//  nms_finish  one workgroup per image: one wave per large class runs the
-//              serial greedy scan over the bitmask (removed words in LDS, one
-//              64-bit OR per lane per kept row), then an exclusive scan of the
-//              per-class kept counts places every kept row in class order.
+//  nms_prep    one 1024-thread workgroup per image: class histogram (LDS
+//              atomics) + exclusive scan -> one bucket per class; every wave
+//              pulls whole classes from an LDS counter and a class of S <= 512
+//              candidates is finished entirely in registers (64*R keys
+//              bitonic-sorted across lanes and register slots, greedy scan with
+//              removed/kept bit masks, box i broadcast by readlane). Larger
+//              classes are queued as tasks for nms_big.
+//  nms_big     one 1024-thread workgroup per large class (grid-strided task
+//              loop). (1) score sort (score desc, row asc = torchvision's stable
+//              descending order) -> rank. (2) spatial counting sort: level =
+//              size octave of max(w, h) relative to the class extent, cell =
+//              centre cell in a 2^L x 2^L grid of that level. (3) per box, the
+//              higher-ranked boxes with IoU > thr ("suppressors") are searched
+//              only where they can exist: IoU > t forces w_j/w_i and h_j/h_i
+//              into (t, 1/t) (so only a few levels qualify) and the boxes to
+//              overlap (so only the cells whose centres lie within half the
+//              level's largest box of this one). (4) greedy resolution as a
+//              parallel fixed point: a box is kept once all its suppressors are
+//              removed, removed once any is kept; every round decides at least
+//              the highest-ranked undecided box, and each decision equals the
+//              greedy one by induction on rank. (5) kept rows compacted in rank
+//              order.
+//  nms_finish  one workgroup per image: exclusive scan of the per-class kept
+//              counts places every kept row in class order; padded outputs.
 //
 // IoU is torchvision's fp32 expression inter / (area_i + area_j - inter),
 // area = (x2-x1)*(y2-y1), compared as (double)iou > iou_threshold; FMA
@@ -34,21 +41,35 @@ namespace {
 constexpr int kThreads = 1024;
 constexpr int kMaxNc = 1024;      // classes handled in LDS
 constexpr int kRegMax = 512;      // largest class finished in registers (R = 8 slots per lane)
-constexpr int kLdsKeys = 8192;    // largest class sorted in LDS
 constexpr int kMaxRows = 131072;  // rows (candidates) per image
-constexpr int kMaskThreads = 256;
-constexpr int kMaskBlocks = 2048;
+constexpr int kBigBlocks = 256;   // nms_big grid (task-strided)
+constexpr int kSlots = 16;        // highest-ranked suppressors cached per box
+constexpr int kLevels = 7;        // size octaves: level L holds max(w, h) < 2^-L of the class extent
+constexpr int kGridCells = 5461;  // sum_{L < 7} 4^L
+constexpr int kWild = kGridCells; // one extra cell: boxes without a finite positive size
+constexpr int kCells = kGridCells + 1;
 
-struct Seg {  // one large class = one task range of nms_mask
-  int img, off, S, nbw;
-  long long mask_off;  // u64 words from the image's mask base
-  int task_start, pad;
+#ifdef YCX_NMS_PROFILE
+// Development counters: shader cycles per nms_big phase, summed over tasks.
+__device__ unsigned long long g_nms_prof[16];
+#define YCX_PROF_MARK(i)                                               \
+  if (tid == 0) {                                                      \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();      \
+    atomicAdd(&g_nms_prof[i], now_ - t_prev_);                         \
+    t_prev_ = now_;                                                    \
+  }
+#else
+#define YCX_PROF_MARK(i)
+#endif
+
+struct Task {  // one large class
+  int img, cls, off, S;
 };
 
 struct Layout {
-  size_t hdr, segs, per_image_base;  // header + segment table (batch), then per image:
-  size_t keys, box, area, bucket, kept, cnt, offs, kc, big, mask, per_image;
-  int max_segs;
+  size_t hdr, tasks, per_image_base;  // header + task table (batch), then per image:
+  size_t keys, bucket, kept, sbox, srank, nsup, slots, state, cnt, offs, kc, per_image;
+  int max_tasks;
 };
 
 __host__ __device__ inline int next_pow2(int v) {
@@ -61,27 +82,30 @@ __host__ __device__ inline size_t al(size_t v) { return (v + 255) & ~(size_t)255
 
 __host__ __device__ inline Layout layout(int n, int rows) {
   Layout L;
-  L.max_segs = rows / (kRegMax + 1) + 1;
+  L.max_tasks = rows / (kRegMax + 1) + 1;
   L.hdr = 0;
-  L.segs = 256;
-  L.per_image_base = al(L.segs + (size_t)n * L.max_segs * sizeof(Seg));
+  L.tasks = 256;
+  L.per_image_base = al(L.tasks + (size_t)n * L.max_tasks * sizeof(Task));
   size_t o = 0;
-  L.keys = o; o = al(o + (size_t)next_pow2(rows) * 8);
-  L.box = o; o = al(o + (size_t)rows * 16);
-  L.area = o; o = al(o + (size_t)rows * 4);
+  // keys: a class at bucket offset `off` with S rows sorts at keys + 2*off; its
+  // power-of-two span is < 2S and off + S <= rows, so 2*rows keys suffice.
+  L.keys = o; o = al(o + (size_t)2 * rows * 8);
   L.bucket = o; o = al(o + (size_t)rows * 4);
   L.kept = o; o = al(o + (size_t)rows * 4);
+  L.sbox = o; o = al(o + (size_t)rows * 16);
+  L.srank = o; o = al(o + (size_t)rows * 4);
+  L.nsup = o; o = al(o + (size_t)rows * 4);
+  L.slots = o; o = al(o + (size_t)rows * kSlots * 4);
+  L.state = o; o = al(o + (size_t)rows);
   L.cnt = o; o = al(o + kMaxNc * 4);
   L.offs = o; o = al(o + kMaxNc * 4);
   L.kc = o; o = al(o + kMaxNc * 4);
-  L.big = o; o = al(o + (size_t)(L.max_segs + 1) * 4);
-  L.mask = o; o = al(o + (size_t)rows * ((rows + 63) / 64) * 8);
   L.per_image = o;
   return L;
 }
 
 struct Hdr {
-  int nseg, ntasks;
+  int ntasks;
 };
 
 // Sort key within a class: score descending (inverted fp32 bits; scores are
@@ -248,27 +272,94 @@ __device__ void block_bitonic(unsigned long long* keys, int P) {
   }
 }
 
+// Workgroup bitonic sort of Pn = E * kThreads keys held in registers (element
+// e = tid*E + i): partners within a thread are exchanged in registers, within
+// a wave by shuffles, and only the strides that cross waves go through LDS.
+template <int E>
+__device__ void sort_regs(unsigned long long (&v)[E], unsigned long long* lds, int Pn) {
+  const int t = threadIdx.x;
+  for (int k = 2; k <= Pn; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j < E) {
+#pragma unroll
+        for (int jj = E / 2; jj >= 1; jj >>= 1) {
+          if (jj != j) continue;
+#pragma unroll
+          for (int i = 0; i < E; ++i) {
+            if (i & jj) continue;
+            const int ip = i | jj;
+            const bool up = ((t * E + i) & k) == 0;
+            const unsigned long long a = v[i], b = v[ip];
+            if ((a > b) == up) { v[i] = b; v[ip] = a; }
+          }
+        }
+      } else if (j < 64 * E) {
+        const int lj = j / E;
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+          const int e = t * E + i;
+          const unsigned long long o = __shfl_xor(v[i], lj);
+          const bool up = (e & k) == 0, lower = (e & j) == 0;
+          const unsigned long long mn = v[i] < o ? v[i] : o, mx = v[i] < o ? o : v[i];
+          v[i] = (lower == up) ? mn : mx;
+        }
+      } else {
+        __syncthreads();  // the previous exchange's reads are done
+#pragma unroll
+        for (int i = 0; i < E; ++i) lds[t * E + i] = v[i];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+          const int e = t * E + i;
+          const unsigned long long o = lds[e ^ j];
+          const bool up = (e & k) == 0, lower = (e & j) == 0;
+          const unsigned long long mn = v[i] < o ? v[i] : o, mx = v[i] < o ? o : v[i];
+          v[i] = (lower == up) ? mn : mx;
+        }
+      }
+    }
+  }
+}
+
+// Sort the keys of one class (bucket order in, rank order out in lds[0, Pn)).
+template <int E>
+__device__ void sort_class(const ycx_cand* __restrict__ ci, const int* bucket, int S, unsigned long long* lds) {
+  unsigned long long v[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = threadIdx.x * E + i;
+    v[i] = e < S ? make_key(ci[bucket[e]]) : ~0ull;
+  }
+  sort_regs<E>(v, lds, E * kThreads);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < E; ++i) lds[threadIdx.x * E + i] = v[i];
+  __syncthreads();
+}
+
 struct Ptrs {
-  unsigned long long* keysg;
-  f32x4* box;
-  float* area;
-  int *bucket, *kept, *cnt, *offs, *kc, *big;
-  unsigned long long* mask;
+  unsigned long long* keys;
+  int *bucket, *kept;
+  f32x4* sbox;
+  int *srank, *nsup, *slots;
+  unsigned char* state;
+  int *cnt, *offs, *kc;
 };
 
 __device__ __forceinline__ Ptrs image_ptrs(char* ws, const Layout& L, int img) {
   char* b = ws + L.per_image_base + (size_t)img * L.per_image;
   Ptrs p;
-  p.keysg = reinterpret_cast<unsigned long long*>(b + L.keys);
-  p.box = reinterpret_cast<f32x4*>(b + L.box);
-  p.area = reinterpret_cast<float*>(b + L.area);
+  p.keys = reinterpret_cast<unsigned long long*>(b + L.keys);
   p.bucket = reinterpret_cast<int*>(b + L.bucket);
   p.kept = reinterpret_cast<int*>(b + L.kept);
+  p.sbox = reinterpret_cast<f32x4*>(b + L.sbox);
+  p.srank = reinterpret_cast<int*>(b + L.srank);
+  p.nsup = reinterpret_cast<int*>(b + L.nsup);
+  p.slots = reinterpret_cast<int*>(b + L.slots);
+  p.state = reinterpret_cast<unsigned char*>(b + L.state);
   p.cnt = reinterpret_cast<int*>(b + L.cnt);
   p.offs = reinterpret_cast<int*>(b + L.offs);
   p.kc = reinterpret_cast<int*>(b + L.kc);
-  p.big = reinterpret_cast<int*>(b + L.big);
-  p.mask = reinterpret_cast<unsigned long long*>(b + L.mask);
   return p;
 }
 
@@ -276,21 +367,20 @@ __device__ __forceinline__ Ptrs image_ptrs(char* ws, const Layout& L, int img) {
 __global__ void __launch_bounds__(kThreads) nms_prep(ycx_nms_desc d, const ycx_cand* __restrict__ cand,
                                                      const int* __restrict__ cand_rows,
                                                      const int* __restrict__ cand_counts, char* ws, Thr thr) {
-  __shared__ unsigned long long s_keys[kLdsKeys];
-  __shared__ int s_cnt[kMaxNc], s_off[kMaxNc], s_fill[kMaxNc], s_kc[kMaxNc], s_big[kMaxNc];
-  __shared__ int s_next, s_nbig;
+  __shared__ int s_cnt[kMaxNc], s_off[kMaxNc], s_fill[kMaxNc], s_kc[kMaxNc];
+  __shared__ int s_next;
   const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nc = d.nc, rows = d.rows_total;
   const Layout L = layout(d.n, rows);
   const Ptrs P = image_ptrs(ws, L, img);
   Hdr* hdr = reinterpret_cast<Hdr*>(ws + L.hdr);
-  Seg* segs = reinterpret_cast<Seg*>(ws + L.segs);
+  Task* tasks = reinterpret_cast<Task*>(ws + L.tasks);
   const ycx_cand* ci = cand + (size_t)img * rows;
   const int* cr = cand_rows + (size_t)img * rows;
   const int cnt = min(cand_counts[img], rows);
 
   for (int c = tid; c < nc; c += kThreads) { s_cnt[c] = 0; s_fill[c] = 0; s_kc[c] = 0; }
-  if (tid == 0) { s_next = 0; s_nbig = 0; }
+  if (tid == 0) s_next = 0;
   __syncthreads();
   for (int i = tid; i < cnt; i += kThreads) atomicAdd(&s_cnt[ci[cr[i]].cls], 1);
   __syncthreads();
@@ -303,7 +393,8 @@ __global__ void __launch_bounds__(kThreads) nms_prep(ycx_nms_desc d, const ycx_c
   }
   __syncthreads();
 
-  // Classes of <= kRegMax candidates: one wave each, in registers.
+  // Classes of <= kRegMax candidates: one wave each, in registers; larger
+  // classes become nms_big tasks.
   for (int it = 0; it <= nc + 64; ++it) {  // bounded work-queue loop
     int c = 0;
     if (lane == 0) c = atomicAdd(&s_next, 1);
@@ -312,7 +403,7 @@ __global__ void __launch_bounds__(kThreads) nms_prep(ycx_nms_desc d, const ycx_c
     const int S = __builtin_amdgcn_readfirstlane(s_cnt[c]);
     if (S == 0) continue;
     if (S > kRegMax) {
-      if (lane == 0) s_big[atomicAdd(&s_nbig, 1)] = c;
+      if (lane == 0) tasks[atomicAdd(&hdr->ntasks, 1)] = Task{img, c, s_off[c], S};
       continue;
     }
     const int* bk = P.bucket + s_off[c];
@@ -323,98 +414,434 @@ __global__ void __launch_bounds__(kThreads) nms_prep(ycx_nms_desc d, const ycx_c
     else class_in_registers<8>(ci, bk, kp, S, thr, &s_kc[c]);
   }
   __syncthreads();
-
-  // Large classes: workgroup sort (LDS keys when they fit), sorted rows back
-  // into the bucket, sorted boxes/areas for nms_mask, one task range queued.
-  const int nbig = s_nbig;
-  long long mask_off = 0;
-  for (int q = 0; q < nbig; ++q) {
-    const int c = s_big[q];
-    const int S = s_cnt[c], off = s_off[c];
-    const int Pn = next_pow2(S);
-    unsigned long long* keys = Pn <= kLdsKeys ? s_keys : P.keysg;
-    for (int i = tid; i < Pn; i += kThreads) keys[i] = i < S ? make_key(ci[P.bucket[off + i]]) : ~0ull;
-    __syncthreads();
-    block_bitonic(keys, Pn);
-    for (int i = tid; i < S; i += kThreads) {
-      const int r = (int)(unsigned)keys[i];
-      const ycx_cand b = ci[r];
-      P.bucket[off + i] = r;
-      P.box[off + i] = f32x4{b.x1, b.y1, b.x2, b.y2};
-      P.area[off + i] = (b.x2 - b.x1) * (b.y2 - b.y1);
-    }
-    const int nbw = (S + 63) / 64;
-    if (tid == 0) {
-      const int sid = atomicAdd(&hdr->nseg, 1);
-      const int t0 = atomicAdd(&hdr->ntasks, nbw);
-      segs[sid] = Seg{img, off, S, nbw, mask_off, t0, 0};
-    }
-    mask_off += (long long)S * nbw;
-    __syncthreads();
-  }
-  // Per-image class tables for nms_finish.
+  // Per-image class tables (nms_big overwrites kc of its classes).
   for (int c = tid; c < nc; c += kThreads) {
     P.cnt[c] = s_cnt[c];
     P.offs[c] = s_off[c];
     P.kc[c] = s_kc[c];
   }
-  for (int q = tid; q < nbig; q += kThreads) P.big[1 + q] = s_big[q];
-  if (tid == 0) P.big[0] = nbig;
 }
 
 // ---------------------------------------------------------------------------
-// One wave per (large class, 64-row strip): rows i = 64*bi + lane against every
-// column block bj >= bi; column boxes are broadcast from registers by readlane.
-__global__ void __launch_bounds__(kMaskThreads) nms_mask(ycx_nms_desc d, char* ws, Thr thr) {
-  const Layout L = layout(d.n, d.rows_total);
-  const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
-  const Seg* segs = reinterpret_cast<const Seg*>(ws + L.segs);
-  // Per-wave LDS slice holding one 64-box column block (boxes + areas); every
-  // lane reads column c by a broadcast ds_read (same address in all lanes).
-  __shared__ f32x4 s_box[kMaskThreads / 64][64];
-  __shared__ float s_area[kMaskThreads / 64][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int nseg = hdr->nseg, ntasks = hdr->ntasks;
-  const int gw = (blockIdx.x * kMaskThreads + threadIdx.x) >> 6;
-  const int nw = gridDim.x * (kMaskThreads >> 6);
-  f32x4* cb = s_box[wv];
-  float* ca = s_area[wv];
-  for (int t = gw; t < ntasks; t += nw) {
-    int s = 0;
-    while (s + 1 < nseg && !(segs[s].task_start <= t && t < segs[s].task_start + segs[s].nbw)) ++s;
-    const Seg sg = segs[s];
-    const Ptrs P = image_ptrs(ws, L, sg.img);
-    const int bi = t - sg.task_start;
-    const int i = bi * 64 + lane;
-    const bool rv = i < sg.S;
-    const f32x4 a = rv ? P.box[sg.off + i] : f32x4{0.f, 0.f, 0.f, 0.f};
-    const float aa = rv ? P.area[sg.off + i] : 0.0f;
-    unsigned long long* mrow = P.mask + sg.mask_off + (long long)i * sg.nbw;
-    // column block bi first (its own rows), then prefetch one block ahead
-    f32x4 nb = a;
-    float na = aa;
-    for (int bj = bi; bj < sg.nbw; ++bj) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // previous block's LDS reads done
-      cb[lane] = nb;
-      ca[lane] = na;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int jn = (bj + 1) * 64 + lane;
-      const bool nv = bj + 1 < sg.nbw && jn < sg.S;
-      nb = nv ? P.box[sg.off + jn] : f32x4{0.f, 0.f, 0.f, 0.f};
-      na = nv ? P.area[sg.off + jn] : 0.0f;
-      const int cmax = min(64, sg.S - bj * 64);  // uniform
-      unsigned lo = 0u, hi = 0u;
-#pragma unroll
-      for (int c = 0; c < 64; ++c) {
-        const f32x4 b = cb[c];
-        const float ba = ca[c];
-        const bool sup = c < cmax && (bj > bi || c > lane) &&
-                         suppress(a[0], a[1], a[2], a[3], aa, b[0], b[1], b[2], b[3], ba, thr);
-        if (c < 32) lo |= sup ? (1u << c) : 0u;
-        else hi |= sup ? (1u << (c - 32)) : 0u;
-      }
-      if (rv) mrow[bj] = ((unsigned long long)hi << 32) | lo;
+// nms_big helpers
+
+// Order-preserving int image of a float (LDS atomicMin/Max on floats).
+__device__ __forceinline__ int f2o(float f) {
+  const int i = __float_as_int(f);
+  return i >= 0 ? i : i ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float o2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
+
+__device__ __forceinline__ int level_base(int L) { return ((1 << (2 * L)) - 1) / 3; }  // sum_{l < L} 4^l
+
+__device__ __forceinline__ int clamp_cell(float v, int G) {
+  return (int)fminf(fmaxf(floorf(v), 0.0f), (float)(G - 1));
+}
+
+// Class-normalised geometry of one box: level = size octave of max(w, h),
+// cell = centre cell of that level's 2^L x 2^L grid; level -1 = irregular
+// (non-finite or non-positive extent: compared against every box).
+struct Geo {
+  float nx1, ny1, nx2, ny2, w, h;
+  int level, cell;
+};
+
+__device__ __forceinline__ Geo geometry(const f32x4 b, float X0, float Y0, float inv, bool all_pairs) {
+  Geo g;
+  g.nx1 = (b[0] - X0) * inv;
+  g.ny1 = (b[1] - Y0) * inv;
+  g.nx2 = (b[2] - X0) * inv;
+  g.ny2 = (b[3] - Y0) * inv;
+  g.w = g.nx2 - g.nx1;
+  g.h = g.ny2 - g.ny1;
+  const float s = fmaxf(g.w, g.h);
+  const bool reg = !all_pairs && g.w > 0.0f && g.h > 0.0f && s < INFINITY && b[0] > -INFINITY && b[1] > -INFINITY;
+  if (!reg) {
+    g.level = -1;
+    g.cell = kWild;
+    return g;
+  }
+  const int e = (int)(__float_as_uint(s) >> 23) - 126;  // s < 2^e
+  const int L = min(max(-e, 0), kLevels - 1);
+  const int G = 1 << L;
+  const int ix = clamp_cell((g.nx1 + g.nx2) * 0.5f * (float)G, G);
+  const int iy = clamp_cell((g.ny1 + g.ny2) * 0.5f * (float)G, G);
+  g.level = L;
+  g.cell = level_base(L) + iy * G + ix;
+  return g;
+}
+
+// Spatially sorted boxes of one large class: in LDS (ranks as u16) when they
+// fit, else in the per-image workspace.
+template <bool kLds>
+struct Ctx {
+  const int* cells;  // LDS: end position of cell k (start = cells[k - 1], 0 for k = 0)
+  const int (*lv)[5];  // LDS: per level count, max w, max h, min w, min h (float bits)
+  const f32x4* sbox;
+  const unsigned short* r16;
+  const int* r32;
+  float t_lo, inv_t;
+  int S;
+  __device__ __forceinline__ int rank(int q) const {
+    if constexpr (kLds) return r16[q];
+    else return r32[q];
+  }
+};
+
+// (x2 - x1) * (y2 - y1): the reference's area expression, bit-identical to the
+// one the candidates were filtered with (contraction is off in this file).
+__device__ __forceinline__ float box_area(const f32x4 b) { return (b[2] - b[0]) * (b[3] - b[1]); }
+
+// The position ranges (cell rows of the compatible levels) that can hold a box
+// with IoU > thr against the box of geometry g; run(q0, q1) returns false to
+// stop. IoU > t forces t < w_j/w_i < 1/t and t < h_j/h_i < 1/t (IoU <= inter/a_j <=
+// w_i h_j/(w_j h_j)) and overlap (centre within half the partner's extent).
+// The ratio tests use t_lo = t(1 - 1e-3) and an absolute slack, the windows a
+// 1e-5 margin, both far above the fp32 rounding of the normalised geometry.
+template <bool kLds, class F>
+__device__ __forceinline__ bool for_ranges(const Ctx<kLds>& c, const Geo& g, F&& run) {
+  if (g.level < 0) return run(0, c.S);
+  if (!run(c.cells[kWild - 1], c.cells[kWild])) return false;
+  constexpr float kSlack = 1e-6f, kEps = 1e-5f;
+  for (int L = 0; L < kLevels; ++L) {
+    if (c.lv[L][0] == 0) continue;
+    const float mw = __int_as_float(c.lv[L][1]), mh = __int_as_float(c.lv[L][2]);
+    const float nw = __int_as_float(c.lv[L][3]), nh = __int_as_float(c.lv[L][4]);
+    if (mw + kSlack < c.t_lo * g.w || mh + kSlack < c.t_lo * g.h) continue;  // all too narrow / too flat
+    if (nw - kSlack > (g.w + kSlack) * c.inv_t || nh - kSlack > (g.h + kSlack) * c.inv_t) continue;  // too big
+    const int G = 1 << L, base = level_base(L);
+    const float Gf = (float)G;
+    const int ix0 = clamp_cell((g.nx1 - 0.5f * mw - kEps) * Gf, G), ix1 = clamp_cell((g.nx2 + 0.5f * mw + kEps) * Gf, G);
+    const int iy0 = clamp_cell((g.ny1 - 0.5f * mh - kEps) * Gf, G), iy1 = clamp_cell((g.ny2 + 0.5f * mh + kEps) * Gf, G);
+    for (int iy = iy0; iy <= iy1; ++iy) {  // cells ix0..ix1 of a grid row are contiguous positions
+      const int k0 = base + iy * G + ix0, k1 = base + iy * G + ix1;
+      if (!run(k0 ? c.cells[k0 - 1] : 0, c.cells[k1])) return false;
     }
+  }
+  return true;
+}
+
+// Visit every spatial position q whose box can have IoU > thr with the box of
+// geometry g (for_ranges) and whose rank is below r; f(q, rank) returns false
+// to stop.
+template <bool kLds, class F>
+__device__ __forceinline__ bool for_candidates(const Ctx<kLds>& c, const Geo& g, int r, F&& f) {
+  return for_ranges(c, g, [&](int q0, int q1) -> bool {
+    for (int q = q0; q < q1; ++q) {
+      const int rj = c.rank(q);
+      if (rj < r && !f(q, rj)) return false;
+    }
+    return true;
+  });
+}
+
+struct Frame {  // per-task values shared by the resolve phases
+  int S, off;
+  float X0, Y0, inv;
+  int all_pairs;
+};
+
+// Phases (4) suppressor search and (5) fixed-point resolution of one class.
+template <bool kLds>
+__device__ void resolve(const Ctx<kLds>& c, const Frame& fr, const Ptrs& P, unsigned char* st, const Thr& thr,
+                        int* s_flag) {
+  const int tid = threadIdx.x, S = fr.S, off = fr.off;
+#ifdef YCX_NMS_PROFILE
+  unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
+#endif
+  // (4) suppressors of every box (spatial order: a wave's boxes share level and
+  // neighbourhood). Each box keeps its kSlots highest-ranked suppressors
+  // (smallest ranks, ascending): they decide most boxes, and a box needs a
+  // rescan only when all of them end up removed while more exist.
+  for (int p = tid; p < S; p += kThreads) {
+    const int r = c.rank(p);
+    const f32x4 b = c.sbox[p];
+    const float a = box_area(b);
+    const Geo g = geometry(b, fr.X0, fr.Y0, fr.inv, fr.all_pairs);
+    int top[kSlots];
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) top[k] = 0x7FFFFFFF;
+    int ns = 0;
+#ifdef YCX_NMS_PROFILE
+    int visits = 0;
+#endif
+    auto test = [&](int rj, const f32x4& o) {
+      // for thr >= 0 a suppressor must overlap (inter > 0): four compares first
+      const bool cand = rj < r && (fr.all_pairs || (o[0] < b[2] && o[2] > b[0] && o[1] < b[3] && o[3] > b[1]));
+      if (cand && suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
+        int v = rj;
+#pragma unroll
+        for (int k = 0; k < kSlots; ++k) {
+          const int lo = min(v, top[k]);
+          v = max(v, top[k]);
+          top[k] = lo;
+        }
+        ++ns;
+      }
+    };
+    for_ranges(c, g, [&](int q0, int q1) {
+#ifdef YCX_NMS_PROFILE
+      visits += q1 - q0;
+#endif
+      int q = q0;
+      for (; q + 4 <= q1; q += 4) {  // four candidates' loads in flight
+        int rj[4];
+        f32x4 o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          rj[u] = c.rank(q + u);
+          o[u] = c.sbox[q + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) test(rj[u], o[u]);
+      }
+      for (; q < q1; ++q) test(c.rank(q), c.sbox[q]);
+      return true;
+    });
+    int* sl = P.slots + (size_t)(off + p) * kSlots;
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k)
+      if (k < ns) sl[k] = top[k];
+    P.nsup[off + p] = ns;
+#ifdef YCX_NMS_PROFILE
+    if (ns > kSlots) atomicAdd(&g_nms_prof[6], 1ull);
+    atomicAdd(&g_nms_prof[8], (unsigned long long)visits);
+    atomicAdd(&g_nms_prof[10], (unsigned long long)ns);
+    int mx = visits;
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+    if ((tid & 63) == 0) atomicAdd(&g_nms_prof[9], (unsigned long long)mx);
+#endif
+  }
+  // (5) greedy as a fixed point over ranks: 0 undecided, 1 kept, 2 removed
+  for (int r = tid; r < S; r += kThreads) st[r] = 0;
+  __syncthreads();
+  YCX_PROF_MARK(2)
+  for (int it = 0; it <= S; ++it) {  // every round decides at least one box
+    if (tid == 0) *s_flag = 0;
+    __syncthreads();
+    int undecided = 0;
+    for (int p = tid; p < S; p += kThreads) {
+      const int r = c.rank(p);
+      if (st[r] != 0) continue;
+      const int ns = P.nsup[off + p];
+      int res = 0;  // 0: every suppressor removed, 1: some undecided, 2: one kept
+      const int* sl = P.slots + (size_t)(off + p) * kSlots;
+      for (int k = 0; k < min(ns, kSlots); ++k) {
+        const unsigned char sj = st[sl[k]];
+        if (sj == 1) { res = 2; break; }
+        if (sj == 0) res = 1;
+      }
+      if (ns > kSlots && res == 0) {  // the cached ones are all removed: look at the rest
+        const f32x4 b = c.sbox[p];
+        const float a = box_area(b);
+        const Geo g = geometry(b, fr.X0, fr.Y0, fr.inv, fr.all_pairs);
+        for_candidates(c, g, r, [&](int q, int rj) {
+          const unsigned char sj = st[rj];
+          if (sj == 2) return true;
+          const f32x4 o = c.sbox[q];
+          if (suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
+            if (sj == 1) { res = 2; return false; }
+            res = 1;
+          }
+          return true;
+        });
+      }
+      if (res == 2) st[r] = 2;
+      else if (res == 0) st[r] = 1;
+      else undecided = 1;
+    }
+    if (undecided) *s_flag = 1;
+    __syncthreads();
+    const int more = *s_flag;
+    __syncthreads();
+#ifdef YCX_NMS_PROFILE
+    if (tid == 0) atomicAdd(&g_nms_prof[5], 1ull);
+#endif
+    if (!more) break;
+  }
+  YCX_PROF_MARK(3)
+}
+
+// Block-wide exclusive scan helper: returns this thread's exclusive prefix of
+// `v` over the workgroup and writes the block total to *total.
+__device__ __forceinline__ int block_exclusive(int v, int* s_w, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const int t = __shfl_up(incl, dd);
+    if (lane >= dd) incl += t;
+  }
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  int pre = 0, tot = 0;
+  for (int w = 0; w < kThreads / 64; ++w) {
+    const int x = s_w[w];
+    pre += w < wid ? x : 0;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + incl - v;
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) nms_big(ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws,
+                                                    Thr thr, float t_lo, float inv_t, int all_pairs) {
+  constexpr int kLdsBytes = 159744;
+  constexpr int kLdsCellBytes = ((kCells * 4) + 255) & ~255;
+  static_assert(kLdsBytes >= 16384 * 8, "LDS keys");
+  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
+  __shared__ int s_lv[kLevels][5];
+  __shared__ int s_ext[4];
+  __shared__ int s_w[kThreads / 64];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x;
+  const int rows = d.rows_total;
+  const Layout L = layout(d.n, rows);
+  const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
+  const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks);
+  const int ntasks = hdr->ntasks;
+  int* cells = reinterpret_cast<int*>(smem);
+  for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
+    const Task tk = tasks[t];
+    const Ptrs P = image_ptrs(ws, L, tk.img);
+    const ycx_cand* ci = cand + (size_t)tk.img * rows;
+    const int S = tk.S, off = tk.off;
+    int* bucket = P.bucket + off;
+#ifdef YCX_NMS_PROFILE
+    unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
+    if (tid == 0) atomicAdd(&g_nms_prof[7], 1ull);
+#endif
+    if (tid == 0) {
+      s_ext[0] = s_ext[1] = 0x7FFFFFFF;  // min x1, min y1
+      s_ext[2] = s_ext[3] = (int)0x80000000;  // max x2, max y2
+    }
+    if (tid < kLevels) {
+      s_lv[tid][0] = 0;
+      s_lv[tid][1] = s_lv[tid][2] = 0;  // +0.0f
+      s_lv[tid][3] = s_lv[tid][4] = 0x7F800000;  // +inf
+    }
+    // (1) rank = position in (score desc, row asc) order
+    const int Pn = max(next_pow2(S), kThreads);
+    unsigned long long* keys =
+        Pn <= kLdsBytes / 8 ? reinterpret_cast<unsigned long long*>(smem) : P.keys + 2 * (size_t)off;
+    switch (Pn / kThreads) {  // uniform
+      case 1: sort_class<1>(ci, bucket, S, keys); break;
+      case 2: sort_class<2>(ci, bucket, S, keys); break;
+      case 4: sort_class<4>(ci, bucket, S, keys); break;
+      case 8: sort_class<8>(ci, bucket, S, keys); break;
+      case 16: sort_class<16>(ci, bucket, S, keys); break;
+      default:  // > 16384 keys: workspace bitonic
+        for (int i = tid; i < Pn; i += kThreads) keys[i] = i < S ? make_key(ci[bucket[i]]) : ~0ull;
+        __syncthreads();
+        block_bitonic(keys, Pn);
+    }
+    YCX_PROF_MARK(0)
+    // (2) bucket in rank order; extent of the class's regular boxes
+    for (int r = tid; r < S; r += kThreads) {
+      const int row = (int)(unsigned)keys[r];
+      bucket[r] = row;
+      const ycx_cand b = ci[row];
+      if (b.x2 > b.x1 && b.y2 > b.y1 && b.x1 > -INFINITY && b.y1 > -INFINITY && b.x2 < INFINITY && b.y2 < INFINITY) {
+        atomicMin(&s_ext[0], f2o(b.x1));
+        atomicMin(&s_ext[1], f2o(b.y1));
+        atomicMax(&s_ext[2], f2o(b.x2));
+        atomicMax(&s_ext[3], f2o(b.y2));
+      }
+    }
+    __syncthreads();  // keys dead from here: LDS becomes the cell table
+    for (int k = tid; k < kCells; k += kThreads) cells[k] = 0;
+    __syncthreads();
+    const float X0 = o2f(s_ext[0]), Y0 = o2f(s_ext[1]);
+    const float E = fmaxf(o2f(s_ext[2]) - X0, o2f(s_ext[3]) - Y0);
+    const float inv = (E > 0.0f && E < INFINITY) ? 1.0f / E : 0.0f;  // 0: every box irregular
+    // (3) spatial counting sort: histogram (cell id parked in nsup[rank]), scan, scatter
+    for (int r = tid; r < S; r += kThreads) {
+      const ycx_cand b = ci[bucket[r]];
+      const Geo g = geometry(f32x4{b.x1, b.y1, b.x2, b.y2}, X0, Y0, inv, all_pairs);
+      P.nsup[off + r] = g.cell;
+      atomicAdd(&cells[g.cell], 1);
+    }
+    // per-level count / extreme sizes: reduced per wave, one LDS atomic per wave and level
+    for (int r0 = 0; r0 < S; r0 += kThreads) {  // uniform trip count
+      const int r = r0 + tid;
+      Geo g;
+      g.level = -1;
+      if (r < S) {
+        const ycx_cand b = ci[bucket[r]];
+        g = geometry(f32x4{b.x1, b.y1, b.x2, b.y2}, X0, Y0, inv, all_pairs);
+      }
+      for (int Lv = 0; Lv < kLevels; ++Lv) {
+        const bool in = g.level == Lv;
+        const unsigned long long m = __ballot(in);
+        if (!m) continue;
+        int mxw = in ? __float_as_int(g.w) : 0, mxh = in ? __float_as_int(g.h) : 0;
+        int mnw = in ? __float_as_int(g.w) : 0x7F800000, mnh = in ? __float_as_int(g.h) : 0x7F800000;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          mxw = max(mxw, __shfl_xor(mxw, o));
+          mxh = max(mxh, __shfl_xor(mxh, o));
+          mnw = min(mnw, __shfl_xor(mnw, o));
+          mnh = min(mnh, __shfl_xor(mnh, o));
+        }
+        if ((tid & 63) == 0) {
+          atomicAdd(&s_lv[Lv][0], __popcll(m));
+          atomicMax(&s_lv[Lv][1], mxw);
+          atomicMax(&s_lv[Lv][2], mxh);
+          atomicMin(&s_lv[Lv][3], mnw);
+          atomicMin(&s_lv[Lv][4], mnh);
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < 64) wave_exclusive_scan(cells, cells, kCells);
+    __syncthreads();
+    // Boxes + u16 ranks + state in LDS when they fit (19 B per box), else the
+    // workspace (state still in LDS up to its size).
+    const bool lds = 19 * S + 32 <= kLdsBytes - kLdsCellBytes;
+    f32x4* lbox = reinterpret_cast<f32x4*>(smem + kLdsCellBytes);
+    unsigned short* lr = reinterpret_cast<unsigned short*>(smem + kLdsCellBytes + 16 * S);
+    unsigned char* st = lds ? reinterpret_cast<unsigned char*>(smem + kLdsCellBytes + 16 * S + ((2 * S + 15) & ~15))
+                            : S <= kLdsBytes - kLdsCellBytes ? reinterpret_cast<unsigned char*>(smem + kLdsCellBytes)
+                                                             : P.state + off;
+    for (int r = tid; r < S; r += kThreads) {
+      const int q = atomicAdd(&cells[P.nsup[off + r]], 1);  // cells[k] ends as the end of cell k
+      const ycx_cand b = ci[bucket[r]];
+      if (lds) {
+        lr[q] = (unsigned short)r;
+        lbox[q] = f32x4{b.x1, b.y1, b.x2, b.y2};
+      } else {
+        P.srank[off + q] = r;
+        P.sbox[off + q] = f32x4{b.x1, b.y1, b.x2, b.y2};
+      }
+    }
+    __syncthreads();
+    YCX_PROF_MARK(1)
+    const Frame fr{S, off, X0, Y0, inv, all_pairs};
+    if (lds) {
+      Ctx<true> c{cells, s_lv, lbox, lr, nullptr, t_lo, inv_t, S};
+      resolve<true>(c, fr, P, st, thr, &s_flag);
+    } else {
+      Ctx<false> c{cells, s_lv, P.sbox + off, nullptr, P.srank + off, t_lo, inv_t, S};
+      resolve<false>(c, fr, P, st, thr, &s_flag);
+    }
+#ifdef YCX_NMS_PROFILE
+    t_prev_ = __builtin_amdgcn_s_memtime();
+#endif
+    // (6) kept rows in rank order
+    int base = 0;
+    for (int r0 = 0; r0 < S; r0 += kThreads) {
+      const int r = r0 + tid;
+      const int k = (r < S && st[r] == 1) ? 1 : 0;
+      int total;
+      const int pos = block_exclusive(k, s_w, &total);
+      if (k) P.kept[off + base + pos] = bucket[r];
+      base += total;
+    }
+    if (tid == 0) P.kc[tk.cls] = base;
+    __syncthreads();
+    YCX_PROF_MARK(4)
   }
 }
 
@@ -422,89 +849,14 @@ __global__ void __launch_bounds__(kMaskThreads) nms_mask(ycx_nms_desc d, char* w
 __global__ void __launch_bounds__(kThreads) nms_finish(ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws,
                                                        float* __restrict__ dets, int* __restrict__ keep_rows,
                                                        int* __restrict__ keep_counts) {
-  __shared__ unsigned long long s_rem[kMaxRows / 64 + 64 * 4];
-  __shared__ int s_kc[kMaxNc], s_koff[kMaxNc], s_off[kMaxNc], s_big[kMaxNc];
-  __shared__ long long s_moff[kMaxNc];
-  __shared__ int s_woff[kMaxNc];
-  __shared__ int s_next, s_total, s_nbig;
+  __shared__ int s_kc[kMaxNc], s_koff[kMaxNc], s_off[kMaxNc];
+  __shared__ int s_total;
   const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nc = d.nc, rows = d.rows_total;
   const Layout L = layout(d.n, rows);
   const Ptrs P = image_ptrs(ws, L, img);
   const ycx_cand* ci = cand + (size_t)img * rows;
   for (int c = tid; c < nc; c += kThreads) { s_kc[c] = P.kc[c]; s_off[c] = P.offs[c]; }
-  if (tid == 0) {
-    const int nbig = P.big[0];
-    s_nbig = nbig;
-    s_next = 0;
-    long long mo = 0;
-    int wo = 0;
-    for (int q = 0; q < nbig; ++q) {  // same order as nms_prep: mask offsets, LDS word offsets
-      const int c = P.big[1 + q];
-      const int S = P.cnt[c];
-      s_big[q] = c;
-      s_moff[q] = mo;
-      s_woff[q] = wo;
-      mo += (long long)S * ((S + 63) / 64);
-      wo += (S + 63) / 64;
-    }
-  }
-  __syncthreads();
-  const int nbig = s_nbig;
-  for (int it = 0; it <= nbig + 16; ++it) {  // bounded work-queue loop: one wave per large class
-    int q = 0;
-    if (lane == 0) q = atomicAdd(&s_next, 1);
-    q = __builtin_amdgcn_readfirstlane(__shfl(q, 0));
-    if (q >= nbig) break;
-    const int c = s_big[q];
-    const int S = __builtin_amdgcn_readfirstlane(P.cnt[c]);
-    const int off = s_off[c], nbw = (S + 63) / 64;
-    unsigned long long* rem = s_rem + s_woff[q];
-    const unsigned long long* mask = P.mask + s_moff[q];
-    for (int w = lane; w < nbw; w += 64) rem[w] = 0ull;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    int nk = 0;
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    for (int b = 0; b < nbw; ++b) {
-      // (a) resolve the 64 rows of block b serially: only the diagonal words
-      //     mask[64b + r][b] matter inside the block; lane r holds row r's word.
-      const int i = b * 64 + lane;
-      const unsigned long long diag = i < S ? mask[(long long)i * nbw + b] : 0ull;
-      unsigned long long wb = rem[b];
-      unsigned long long kb = 0ull;
-      const int rmax = min(64, S - b * 64);
-      for (int r = 0; r < rmax; ++r) {
-        if ((wb >> r) & 1ull) continue;
-        kb |= 1ull << r;
-        const unsigned lo = __builtin_amdgcn_readlane((unsigned)diag, r);
-        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(diag >> 32), r);
-        wb |= ((unsigned long long)hi << 32) | lo;
-      }
-      if ((kb >> lane) & 1ull) P.kept[off + nk + __popcll(kb & lt)] = P.bucket[off + i];
-      nk += __popcll(kb);
-      // (b) propagate the kept rows of block b to every later word, 8 independent
-      //     row loads in flight per lane.
-      for (int w = b + 1 + lane; w < nbw; w += 64) {
-        unsigned long long acc = 0ull, m = kb;
-        for (int g = 0; g < 64 && m; g += 8) {
-          int rr[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            rr[u] = m ? __builtin_ctzll(m) : -1;
-            m = m ? (m & (m - 1ull)) : 0ull;
-          }
-          unsigned long long v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = rr[u] >= 0 ? mask[(long long)(b * 64 + rr[u]) * nbw + w] : 0ull;
-#pragma unroll
-          for (int u = 0; u < 8; ++u) acc |= v[u];
-        }
-        rem[w] |= acc;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    }
-    if (lane == 0) s_kc[c] = nk;
-  }
   __syncthreads();
   if (wid == 0) {
     const int total = wave_exclusive_scan(s_kc, s_koff, nc);
@@ -552,6 +904,17 @@ Thr make_thr(double thr) {
 
 }  // namespace
 
+#ifdef YCX_NMS_PROFILE
+extern "C" int ycx_nms_prof_read(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nms_prof), sizeof(g_nms_prof)) != hipSuccess) return 1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_nms_prof), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
+
 extern "C" size_t ycx_nms_workspace_size(const ycx_nms_desc* d) {
   if (!d || d->n <= 0 || d->rows_total <= 0) return 0;
   const Layout L = layout(d->n, d->rows_total);
@@ -569,8 +932,13 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   if (hipMemsetAsync(workspace, 0, 256, st) != hipSuccess) return YCX_ERR_LAUNCH;  // task-queue header
   char* ws = reinterpret_cast<char*>(workspace);
   const Thr t = make_thr(d->iou_thres);
+  // Spatial pruning needs IoU > thr to imply overlap and bounded size ratios,
+  // i.e. thr >= 0; a negative or NaN threshold compares every pair.
+  const int all_pairs = !(d->iou_thres >= 0.0);
+  const float t_lo = all_pairs ? 0.0f : (float)(fmin(d->iou_thres, 1.0) * (1.0 - 1e-3));
+  const float inv_t = t_lo > 0.0f ? 1.0f / t_lo : INFINITY;
   hipLaunchKernelGGL(nms_prep, dim3(d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws, t);
-  hipLaunchKernelGGL(nms_mask, dim3(kMaskBlocks), dim3(kMaskThreads), 0, st, *d, ws, t);
+  hipLaunchKernelGGL(nms_big, dim3(kBigBlocks), dim3(kThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
   hipLaunchKernelGGL(nms_finish, dim3(d->n), dim3(kThreads), 0, st, *d, cand, ws, dets, keep_rows, keep_counts);
   return ycx_launch_status();
 }
