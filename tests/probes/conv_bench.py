@@ -67,7 +67,9 @@ def run(shape, tile, iters=20):
 
 if __name__ == "__main__":
     tiles = [int(t) for t in sys.argv[1:]] or [0]
-    for sh in SHAPES:
+    only = os.environ.get("CONV_SHAPES")  # e.g. "3,4": indices into SHAPES
+    shapes = [SHAPES[int(i)] for i in only.split(",")] if only else SHAPES
+    for sh in shapes:
         row = [str(sh)]
         for t in tiles:
             r = run(sh, t)

@@ -295,6 +295,48 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
   }
 }
 
+// Epilogue from MFMA accumulators (D[co][px]: px = lane & 15, co = 4(lane>>4) + r
+// within each 16x16 fragment): bias + act (+ residual, x2 upsample, fp32 NCHW
+// heads) stored straight from registers.
+template <int FM, int FN>
+__device__ __forceinline__ void epilogue_regs(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob, int pxb,
+                                              int lane) {
+  if (a.out_layout == YCX_OUT_NCHW_F32) {
+    float* Y = reinterpret_cast<float*>(a.y);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        int p = pxb + j * 16 + (lane & 15);
+        if (p >= a.M) continue;
+        int n = p / a.HoWo, rem = p - n * a.HoWo;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int co = cob + i * 16 + (lane >> 4) * 4 + r;
+          if (co < a.Cout)
+            Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] =
+                ycx_act<true>(acc[i][j][r] + a.bias[co], a.act, a.slope);
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int co = cob + i * 16 + (lane >> 4) * 4;
+    if (co >= a.Cout) continue;  // cout % 8 == 0, co % 4 == 0: the 4 channels are all valid
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.bias + co);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int p = pxb + j * 16 + (lane & 15);
+      if (p >= a.M) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = ycx_act<true>(acc[i][j][r] + bv[r], a.act, a.slope);
+      store4_bf16(a, p, co, v);
+    }
+  }
+}
+
 // -------------------------------------------------------------------------
 // bf16 MFMA kernel v2: 512 threads (8 waves), BK = 64, 3-stage LDS-DMA
 // pipeline. Tiles are filled by global_load_lds_dwordx4 (no VGPR staging, no
@@ -444,41 +486,7 @@ __global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  // Epilogue: bias + act (+ residual) straight from the accumulators.
-  if (a.out_layout == YCX_OUT_NCHW_F32) {
-    float* Y = reinterpret_cast<float*>(a.y);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        int p = px0 + wn * TN + j * 16 + (lane & 15);
-        if (p >= a.M) continue;
-        int n = p / a.HoWo, rem = p - n * a.HoWo;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int co = co0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
-          if (co < a.Cout)
-            Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] =
-                ycx_act<true>(acc[i][j][r] + a.bias[co], a.act, a.slope);
-        }
-      }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int co = co0 + wm * TM + i * 16 + (lane >> 4) * 4;
-    if (co >= a.Cout) continue;  // cout % 8 == 0, co % 4 == 0: the 4 channels are all valid
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.bias + co);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int p = px0 + wn * TN + j * 16 + (lane & 15);
-      if (p >= a.M) continue;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = ycx_act<true>(acc[i][j][r] + bv[r], a.act, a.slope);
-      store4_bf16(a, p, co, v);
-    }
-  }
+  epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
 }
 
 // -------------------------------------------------------------------------
