@@ -47,6 +47,8 @@ def parse(argv=None):
     ap.add_argument("--nc", type=int, default=80)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="run each batch's forward and post back to back on one stream")
     ap.add_argument("--conf", type=float, default=0.3)
     ap.add_argument("--iou", type=float, default=0.3)
     ap.add_argument("--max-det", type=int, default=300)
@@ -131,11 +133,11 @@ def cpu_baseline(args, sd, model_cfg, budget_s):
                        f"torch {torch.__version__} CPU, {cores} threads")
 
 
-def setup(args, dev, rank=0, use_graph=None):
+def setup(args, dev, rank=0, use_graph=None, pipeline=False):
     """The bench workload on ``dev``: yolov7 with seeded synthetic weights, a
-    Detector for (batch, 3, size, size) and this rank's synthetic images
-    already resident in HBM."""
-    from ycx.detect import Detector
+    Detector (or a 2-slot PipelinedDetector) for (batch, 3, size, size) and
+    this rank's synthetic images already resident in HBM."""
+    from ycx.detect import Detector, PipelinedDetector
     from ycx.nets.yolo import Model
     from ycx.utils.helper_io import cvt_cfg
     from ycx.utils.synth import synthetic_images, synthetic_state_dict
@@ -146,9 +148,16 @@ def setup(args, dev, rank=0, use_graph=None):
     model.load_state_dict(sd)
     model.to(dev)
     shape = (args.batch, 3, args.size, args.size)
-    det = Detector(model, shape, dev, ANCHORS, MASK, conf_thres=args.conf, nms_thres=args.iou,
-                   max_det=args.max_det, use_graph=(not args.no_graph) if use_graph is None else use_graph)
-    det.x.copy_(synthetic_images(*shape, seed=1000 + rank).to(dev))
+    kw = dict(conf_thres=args.conf, nms_thres=args.iou, max_det=args.max_det,
+              use_graph=(not args.no_graph) if use_graph is None else use_graph)
+    images = synthetic_images(*shape, seed=1000 + rank).to(dev)
+    if pipeline:
+        det = PipelinedDetector(model, shape, dev, ANCHORS, MASK, depth=2, **kw)
+        for d in det.slots:
+            d.x.copy_(images)
+    else:
+        det = Detector(model, shape, dev, ANCHORS, MASK, **kw)
+        det.x.copy_(images)
     return model, det, sd, cfg, shape
 
 
@@ -178,40 +187,57 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    model, det, sd, cfg, shape = setup(args, dev, rank)
+    pipeline = not args.no_pipeline
+    model, det, sd, cfg, shape = setup(args, dev, rank, pipeline=pipeline)
     from ycx.dist import gather_detections
+    lat_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
 
-    def step():
+    def step(i=None):
+        timing = lat_ev[i] if i is not None else None
+        if pipeline:
+            dets, keep, kc, _ = det.submit(timing=timing)
+            if world > 1:  # the single collective, on the post stream after this batch's NMS
+                with torch.cuda.stream(det.s_post):
+                    dets, kc, keep = gather_detections(dets, kc, keep)
+            return kc
+        if timing is not None:
+            timing[0].record()
         dets, keep, kc = det()
         if world > 1:  # the single collective: all-gather of padded detections (+ counts, keep rows)
             dets, kc, keep = gather_detections(dets, kc, keep)
+        if timing is not None:
+            timing[1].record()
         return kc
+
+    def drain():
+        if pipeline:
+            det.synchronize()
+        torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    evs[0].record()
     for i in range(args.steps):
-        kc = step()
-        evs[i + 1].record()
-    torch.cuda.synchronize()
+        kc = step(i)
+    drain()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    lat = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    lat = [a.elapsed_time(b) for a, b in lat_ev]
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     images = world * args.batch * args.steps
     value = images / elapsed
+    det1 = det.slots[0] if pipeline else det
 
-    rl = roofline(det, args.roofline_steps, args.precision) if rank == 0 else None
+    rl = roofline(det1, args.roofline_steps, args.precision) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, sd, cfg, args.cpu_seconds)
@@ -227,6 +253,7 @@ def main():
                                    f"per step: forward + decode + NMS (+ all-gather)",
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch, "image_size": args.size,
                        "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
+                       "pipelined_streams": pipeline,
                        "conf_thres": args.conf, "iou_thres": args.iou, "max_det": args.max_det},
             "mfma_fraction_whole_step": round(model.engine_for(shape, dev).flops_per_image * value /
                                               (world * peak * 1e12), 4),

@@ -11,7 +11,7 @@ import torch
 
 from helpers import ANCHORS, MASK, g3_heads, make_model, rel_err
 from oracle import ref_forward, ref_post
-from ycx.detect import Detector, decode_box, nms_device, non_max_suppression
+from ycx.detect import Detector, PipelinedDetector, decode_box, nms_device, non_max_suppression
 from ycx.utils.helper_io import cvt_cfg
 from ycx.utils.synth import synthetic_images
 
@@ -143,6 +143,27 @@ def test_detector_graph_matches_eager(device):
     d2, k2, c2 = [t.clone() for t in g.post()]
     torch.cuda.synchronize()
     assert torch.equal(c1, c2) and torch.equal(k1, k2) and torch.equal(d1, d2)
+
+
+def test_pipelined_detector_matches_serial(device):
+    """Two slots on two streams, five batches in flight back to back: every
+    batch's detections equal the single-stream Detector's on the same images."""
+    m, _ = make_model('yolov7-tiny', 1, 0, 'bf16')
+    m.to(device)
+    shape = (2, 3, 256, 256)
+    ref = Detector(m, shape, device, ANCHORS, MASK, use_graph=True)
+    pd = PipelinedDetector(m, shape, device, ANCHORS, MASK, depth=2, use_graph=True)
+    xs = [synthetic_images(*shape, seed=20 + i).to(device) for i in range(5)]
+    want = [[t.clone() for t in ref(x)] for x in xs]
+    got = []
+    for x in xs:
+        dets, keep, kc, done = pd.submit(x)
+        torch.cuda.current_stream().wait_event(done)
+        got.append([dets.clone(), keep.clone(), kc.clone()])
+    pd.synchronize()
+    torch.cuda.synchronize()
+    for (d1, k1, c1), (d2, k2, c2) in zip(want, got):
+        assert torch.equal(c1, c2) and torch.equal(k1, k2) and torch.equal(d1, d2)
 
 
 def _check_keep(pred, nc, conf, thr):

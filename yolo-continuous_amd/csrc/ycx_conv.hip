@@ -700,7 +700,13 @@ __global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
     for (int r = 0; r < 4; ++r) bias[t][r] = a.bias[stem_ch(t, 4 * kq + r)];
   const int ngroups = a.M / 16;
   char* __restrict__ Y = reinterpret_cast<char*>(a.y);
-  for (int g = blockIdx.x * 4 + wv; g < ngroups; g += gridDim.x * 4) {
+  // Each workgroup owns a contiguous run of 16-pixel groups, and consecutive
+  // runs sit on one XCD (bijective remap): the three input rows a run reads
+  // are fetched into one L2 instead of every XCD's.
+  const int per = (ngroups + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int g0 = ycx_xcd_remap(blockIdx.x, gridDim.x) * per;
+  const int g1 = min(ngroups, g0 + per);
+  for (int g = g0 + wv; g < g1; g += 4) {
     const int p0 = g * 16;  // scalar: the run lies in one output row
     const int n = p0 / a.HoWo, rem = p0 - n * a.HoWo, oy = rem / a.Wo, ox0 = rem - oy * a.Wo;
     const float* Xn = X + (size_t)(n * a.in_cs + a.in_coff) * HW;

@@ -156,9 +156,9 @@ class Detector:
     [sum na*H*W] candidates, -1 padded), keep_counts [n] (uncapped)."""
 
     def __init__(self, model, shape, device, anchors, anchors_mask, image_size=None, conf_thres=0.3,
-                 nms_thres=0.3, max_det=300, use_graph=True):
+                 nms_thres=0.3, max_det=300, use_graph=True, slot=0):
         self.model = model
-        self.engine = model.engine_for(shape, device)
+        self.engine = model.engine_for(shape, device, slot)
         self.device = torch.device(device)
         n, _, H, W = shape
         image_size = image_size or (H, W)
@@ -204,14 +204,69 @@ class Detector:
                                    self.keep.data_ptr(), self.kc.data_ptr(), st), "ycx_sort_nms")
         return self.dets, self.keep, self.kc
 
-    def __call__(self, images=None, events=None):
-        if images is not None:
-            self.x.copy_(images)
+    def forward(self, events=None):
+        """The model forward on the static input buffer (current stream)."""
         if self.use_graph and events is None:
             self.engine.replay()
         else:
             self.engine.run_static(events)
+        return self.heads
+
+    def __call__(self, images=None, events=None):
+        if images is not None:
+            self.x.copy_(images)
+        self.forward(events)
         return self.post()
+
+
+class PipelinedDetector:
+    """Batches in flight on two HIP streams: while batch i's decode + NMS runs
+    on the post stream, batch i+1's forward already runs on the forward stream.
+    ``depth`` Detector slots (own activation buffers, heads and NMS workspace)
+    rotate; a slot's forward waits for the previous post that read its heads.
+
+    submit(images) enqueues one batch and returns (dets, keep_rows,
+    keep_counts, done_event); the tensors are valid once done_event completes
+    (``synchronize()`` or ``torch.cuda.current_stream().wait_event(done)``)."""
+
+    def __init__(self, model, shape, device, anchors, anchors_mask, depth=2, **kw):
+        self.device = torch.device(device)
+        self.slots = [Detector(model, shape, device, anchors, anchors_mask, slot=k, **kw) for k in range(depth)]
+        # different priorities come from different stream pools and so land on
+        # different hardware queues (two same-pool streams may share one)
+        self.s_fwd = torch.cuda.Stream(self.device, priority=0)
+        self.s_post = torch.cuda.Stream(self.device, priority=-1)
+        self.fwd_done = [torch.cuda.Event() for _ in self.slots]
+        self.post_done = [torch.cuda.Event() for _ in self.slots]
+        self.i = 0
+
+    def submit(self, images=None, timing=None):
+        """``timing`` = (start, end) timing events: recorded when the batch's
+        forward starts and when its detections are complete."""
+        k = self.i % len(self.slots)
+        self.i += 1
+        det = self.slots[k]
+        self.s_fwd.wait_stream(torch.cuda.current_stream(self.device))  # caller's inputs are ready
+        with torch.cuda.stream(self.s_fwd):
+            self.s_fwd.wait_event(self.post_done[k])  # the slot's heads were consumed
+            if timing is not None:
+                timing[0].record(self.s_fwd)
+            if images is not None:
+                det.x.copy_(images)
+            det.forward()
+            self.fwd_done[k].record(self.s_fwd)
+        with torch.cuda.stream(self.s_post):
+            self.s_post.wait_event(self.fwd_done[k])
+            dets, keep, kc = det.post()
+            self.post_done[k].record(self.s_post)
+            if timing is not None:
+                timing[1].record(self.s_post)
+        return dets, keep, kc, self.post_done[k]
+
+    def synchronize(self):
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_stream(self.s_fwd)
+        cur.wait_stream(self.s_post)
 
 
 def prepare_model(plan, weights=None, device=None, precision='bf16'):

@@ -399,6 +399,8 @@ class Engine:
         self.n_ops = len(ops)
         self.ops = (L.Op * max(1, self.n_ops))(*ops)
         self.fixed_outputs = None
+        self.static_input = None
+        self._static_bound = False
 
     def _val_ptr(self, v, op_index, field):
         if v.role == 'input':
@@ -494,13 +496,14 @@ class Engine:
 
     # ------------------------------------------------------------------
     def _alloc_outputs(self):
-        outs = []
-        for v in self.out_vals:
-            t = torch.empty((v.n, v.c, v.h, v.w), dtype=torch.float32, device=self.device)
+        outs = [torch.empty((v.n, v.c, v.h, v.w), dtype=torch.float32, device=self.device) for v in self.out_vals]
+        self._bind_outputs(outs)
+        return outs
+
+    def _bind_outputs(self, outs):
+        for v, t in zip(self.out_vals, outs):
             for idx, field in self.output_slots.get(id(v), []):
                 setattr(self.ops[idx], field, t.data_ptr())
-            outs.append(t)
-        return outs
 
     def _bind_input(self, x):
         if x.device != self.device or x.dtype != torch.float32 or not x.is_contiguous():
@@ -518,6 +521,7 @@ class Engine:
         """Eager forward: fresh output tensors every call (like the reference)."""
         x = self._bind_input(x)
         outs = self._alloc_outputs()
+        self._static_bound = False  # the op array now points at this call's tensors
         ev = None
         if events is not None:
             ev = (ctypes.c_void_p * (self.n_ops + 1))(*[e.cuda_event for e in events])
@@ -527,12 +531,23 @@ class Engine:
 
     # ---- static-I/O path for benchmarking / serving loops ----
     def bind_static(self, x):
-        """Pin the plan to persistent input/output tensors (required by capture())."""
-        self.static_input = self._bind_input(x)
-        self.fixed_outputs = self._alloc_outputs()
+        """Pin the plan to persistent input/output tensors (required by capture()).
+        Idempotent: every caller of one engine shares the same static tensors
+        (and the HIP graph captured on them)."""
+        if self.fixed_outputs is None:
+            self.static_input = self._bind_input(x)
+            self.fixed_outputs = self._alloc_outputs()
+            self._static_bound = True
         return self.static_input, self._result(self.fixed_outputs)
 
+    def _ensure_static(self):
+        if not self._static_bound:  # an eager run() re-pointed the op array
+            self._bind_input(self.static_input)
+            self._bind_outputs(self.fixed_outputs)
+            self._static_bound = True
+
     def run_static(self, events=None):
+        self._ensure_static()
         ev = None
         if events is not None:
             ev = (ctypes.c_void_p * (self.n_ops + 1))(*[e.cuda_event for e in events])
@@ -544,6 +559,7 @@ class Engine:
         if self.fixed_outputs is None:
             raise RuntimeError("ycx: call bind_static() before capture()")
         if self.graph_exec is None:
+            self._ensure_static()
             h = ctypes.c_void_p()
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))

@@ -203,11 +203,13 @@ class Model(nn.Module):
             eng.close()
         self._engines = {}
 
-    def engine_for(self, shape, device):
+    def engine_for(self, shape, device, slot=0):
+        """The compiled plan for (shape, device, precision); ``slot`` > 0 gives an
+        independent copy (own activation buffers) for pipelined execution."""
         from ..engine import Engine
         shape = tuple(int(s) for s in shape)
         dev = torch.device(device)
-        key = (shape, str(dev), self.precision)
+        key = (shape, str(dev), self.precision, int(slot))
         eng = self._engines.get(key)
         if eng is None:
             eng = Engine(self, shape, dev, self.precision)
