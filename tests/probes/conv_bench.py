@@ -25,6 +25,8 @@ SHAPES = [  # n, h, w, cin, cout, k, s
     (32, 160, 160, 256, 128, 1, 1),
     (32, 320, 320, 64, 128, 3, 2),
     (32, 80, 80, 256, 255, 1, 1),
+    (32, 80, 80, 128, 256, 3, 1),
+    (32, 80, 80, 64, 64, 3, 1),
 ]
 
 
@@ -36,7 +38,7 @@ def run(shape, tile, iters=20):
     cpad = 64 if cout <= 64 else -(-cout // 128) * 128
     if tile == 11:
         cpad = -(-cout // 256) * 256
-    if tile in (1, 4, 7, 9, 12, 14, 16) and cpad % 128:
+    if tile in (1, 4, 7, 9, 12, 14, 16, 20, 21) and cpad % 128:
         return None
     x = torch.randn(n, h, w, cin, device=dev).to(torch.bfloat16)
     wt = (torch.randn(cpad, k * k * cin, device=dev) * 0.05).to(torch.bfloat16)

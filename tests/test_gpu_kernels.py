@@ -83,6 +83,24 @@ def test_conv_bf16_tiles(device, tile, cout, cin, k, s):
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize('tile,cin,cout', [(19, 64, 64), (19, 128, 192), (20, 64, 128), (20, 128, 256),
+                                           (21, 192, 128), (21, 64, 256)])
+@pytest.mark.parametrize('hw', [(16, 16), (32, 48)])
+def test_conv_halo3x3(device, tile, cin, cout, hw):
+    """LDS halo-tile 3x3/s1 kernel: image borders are the halo's zero padding,
+    several 64-channel chunks re-fill the halo, channel-sliced input/output."""
+    got, ref = _run_conv(device, 2, hw[0], hw[1], cin, cout, 3, 1, L.ACT_SILU, tile, L.DT_BF16, in_extra=8,
+                         out_extra=16)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+
+
+def test_conv_halo3x3_residual_up2(device):
+    got, ref = _run_conv(device, 1, 32, 16, 64, 64, 3, 1, L.ACT_LEAKY, 19, L.DT_BF16, residual=True)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=2e-2)
+    got, ref = _run_conv(device, 1, 16, 32, 128, 128, 3, 1, L.ACT_SILU, 20, L.DT_BF16, layout=L.OUT_NHWC_UP2)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+
+
 @pytest.mark.parametrize('cin,cout,k,s', [(32, 64, 3, 1), (64, 128, 3, 2), (128, 255, 1, 1), (64, 32, 1, 1)])
 def test_conv_f32(device, cin, cout, k, s):
     layout = L.OUT_NCHW_F32 if cout == 255 else L.OUT_NHWC

@@ -337,6 +337,25 @@ __device__ __forceinline__ void epilogue_regs(const ConvArgs& a, const f32x4 (&a
   }
 }
 
+// Same, for fragments whose 16 pixels start at arbitrary pixel indices pxf[j].
+template <int FM, int FN>
+__device__ __forceinline__ void epilogue_frag(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob,
+                                              const int (&pxf)[FN], int lane) {
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int co = cob + i * 16 + (lane >> 4) * 4;
+    if (co >= a.Cout) continue;
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.bias + co);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = ycx_act<true>(acc[i][j][r] + bv[r], a.act, a.slope);
+      store4_bf16(a, pxf[j] + (lane & 15), co, v);
+    }
+  }
+}
+
 // -------------------------------------------------------------------------
 // bf16 MFMA kernel v2: 512 threads (8 waves), BK = 64, 3-stage LDS-DMA
 // pipeline. Tiles are filled by global_load_lds_dwordx4 (no VGPR staging, no
@@ -487,6 +506,127 @@ __global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
     __builtin_amdgcn_sched_barrier(0);
   }
   epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+}
+
+// -------------------------------------------------------------------------
+// 3x3 stride-1 conv from an LDS halo tile. A block owns a 16x16 output tile of
+// one image and BM output channels. Per 64-channel input chunk the (16+2)^2
+// halo (41.5 KB) is DMA'd into LDS ONCE and all nine taps build their B
+// fragments from it (the im2col path re-fetches every input pixel nine
+// times); the weights of one (tap, chunk) step, BM x 64, stream through
+// NSTA LDS-DMA stages. Halo pixel h keeps its 16-B channel chunk q at slot
+// q ^ (h & 7): the MFMA B reads (16 consecutive pixels x 4 chunk groups) hit
+// 16 distinct bank slots per LDS cycle (brute-forced over every halo offset).
+// Requires H == Ho, W == Wo, Ho % 16 == Wo % 16 == 0, Cin % 64 == 0.
+// -------------------------------------------------------------------------
+template <int BM, int WM, int WN, int NSTA>
+__global__ void __launch_bounds__(WM * WN * 64) conv3x3_halo(ConvArgs a) {
+  constexpr int NW = WM * WN;
+  constexpr int TH = 16, TW = 16, HW = TW + 2, HP = (TH + 2) * HW;  // 324 halo pixels
+  constexpr int HPIECES = (HP + 7) / 8;                             // 1-KB DMA pieces (8 pixels)
+  constexpr int HPW = (HPIECES + NW - 1) / NW;                      // pieces per wave
+  constexpr int TM = BM / WM, FM = TM / 16;
+  constexpr int FN = TH / WN;  // tile rows (16-pixel fragments) per wave
+  constexpr int A_BYTES = BM * 64 * 2, A_PW = BM / (8 * NW);
+  static_assert(A_PW >= 1 && BM % (8 * NW) == 0, "A rows per wave");
+  __shared__ __attribute__((aligned(1024))) char smem[NSTA * A_BYTES + HPIECES * 1024];
+  char* halo = smem + NSTA * A_BYTES;
+
+  const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
+  const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
+  const int ct = L % a.n_ct, rest = L / a.n_ct;
+  const int tx_n = a.Wo / TW, tpi = (a.Ho / TH) * tx_n;
+  const int n = rest / tpi, ti = rest - n * tpi;
+  const int oy0 = (ti / tx_n) * TH, ox0 = (ti % tx_n) * TW, co0 = ct * BM;
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int w_bytes = a.Cout_pad * a.Ktot * 2, x_bytes = a.N * a.H * a.W * a.in_cs * 2;
+
+  int a_off[A_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int row = 8 * (wid + NW * i) + lrow;
+    a_off[i] = ((co0 + row) * a.Ktot + ((pch ^ swz<64>(row)) << 3)) * 2;
+  }
+  int h_off[HPW];  // halo piece i of this wave: byte offset of the lane's chunk (chunk 0 of the tap), or -1
+#pragma unroll
+  for (int i = 0; i < HPW; ++i) {
+    const int h = 8 * (wid + NW * i) + lrow;
+    const int hy = h / HW, hx = h - hy * HW;
+    const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
+    const bool ok = h < HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+    h_off[i] = ok ? (((n * a.H + iy) * a.W + ix) * a.in_cs + a.in_coff + ((pch ^ (h & 7)) << 3)) * 2 : -1;
+  }
+  const int nchunk = a.Cin / 64, total = 9 * nchunk;
+  auto issue_a = [&](int s) {
+    const int c = s / 9, t = s - 9 * c;
+    char* base = smem + (s % NSTA) * A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i)
+      buf_lds16(Wt, w_bytes, a_off[i], (t * a.Cin + 64 * c) * 2, base + (wid + NW * i) * 1024);
+  };
+  auto issue_h = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < HPW; ++i)
+      if (wid + NW * i < HPIECES)
+        buf_lds16(X, x_bytes, h_off[i] >= 0 ? h_off[i] + 128 * c : 0x7FFFFFF0, 0, halo + (wid + NW * i) * 1024);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_h(0);
+#pragma unroll
+  for (int q = 0; q < NSTA - 1; ++q)
+    if (q < total) issue_a(q);
+  for (int s = 0; s < total; ++s) {
+    const int c = s / 9, t = s - 9 * c;
+    if (t == 0 && c > 0) {
+      // next input chunk: every wave is past the previous chunk's last tap, then one halo refill
+      __builtin_amdgcn_s_barrier();
+      issue_h(c);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (NSTA == 3 && s + 1 < total) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_PW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + NSTA - 1 < total) issue_a(s + NSTA - 1);
+    const char* As = smem + (s % NSTA) * A_BYTES;
+    const int ky = t / 3, kx = t - 3 * ky;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int lc = kk * 4 + (lane >> 4);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * TM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + row * 128 + ((lc ^ swz<64>(row)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int h = (wn * FN + j + ky) * HW + (lane & 15) + kx;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(halo + h * 128 + ((lc ^ (h & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  int pxf[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) pxf[j] = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0;
+  epilogue_frag<FM, FN>(a, acc, co0 + wm * TM, pxf, lane);
 }
 
 // -------------------------------------------------------------------------
@@ -777,6 +917,9 @@ const TileInfo kTiles[] = {
     {128, 128, 64, "glds_co128_px128_k64_s2"},
     {64, 256, 32, "glds2_co64_px256_k32x2_s2"},
     {64, 128, 64, "glds_co64_px128_k64_s2"},
+    {64, 256, 64, "halo3x3_co64_t16x16"},
+    {128, 256, 64, "halo3x3_co128_t16x16_s2"},
+    {128, 256, 64, "halo3x3_co128_t16x16_s3"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -787,6 +930,17 @@ ycx_status launch_bf16(ConvArgs a, hipStream_t st) {
   int n_pt = (a.M + BN - 1) / BN;
   a.nwg = a.n_ct * n_pt;
   hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, BK, WM, WN>), dim3(a.nwg), dim3(256), 0, st, a);
+  return ycx_launch_status();
+}
+
+template <int BM, int WM, int WN, int NSTA>
+ycx_status launch_halo(ConvArgs a, hipStream_t st) {
+  if (a.KH != 3 || a.KW != 3 || a.S != 1 || a.P != 1 || a.H != a.Ho || a.W != a.Wo || a.Ho % 16 || a.Wo % 16 ||
+      a.Cin % 64 || a.Cout_pad % BM || a.out_layout == YCX_OUT_NCHW_F32)
+    return YCX_ERR_UNSUPPORTED;
+  a.n_ct = a.Cout_pad / BM;
+  a.nwg = a.n_ct * a.N * (a.Ho / 16) * (a.Wo / 16);
+  hipLaunchKernelGGL((conv3x3_halo<BM, WM, WN, NSTA>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
   return ycx_launch_status();
 }
 
@@ -830,6 +984,13 @@ extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {
     return 5;
   }
   if (!fits) return d->cout_pad % 128 == 0 ? 1 : 2;
+  // 3x3 stride-1 'same' convs on 16-aligned maps: LDS halo tiles (tests/probes/conv_bench.py:
+  // +14-18 % over the im2col tiles at 80^2 with >= 128 output channels, +18 % at 320^2 x 64)
+  if (d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->h == d->ho && d->w == d->wo &&
+      d->ho % 16 == 0 && d->wo % 16 == 0 && d->out_layout != YCX_OUT_NCHW_F32) {
+    if (d->cout_pad % 128 == 0) return 20;
+    if (d->cout_pad == 64 && d->ho >= 160) return 19;
+  }
   if (d->cout_pad % 128 == 0) {
     if ((d->cout_pad / 128) * ((M + 127) / 128) >= 256) return 16;
     return 4;  // co128 x px64, 256 threads: more blocks for small-M (deep) layers
@@ -894,6 +1055,9 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
     case 16: return launch_glds<128, 128, 2, 4, false, 2>(a, st);
     case 17: return launch_glds<64, 256, 1, 8, true, 2>(a, st);
     case 18: return launch_glds<64, 128, 1, 8, false, 2>(a, st);
+    case 19: return launch_halo<64, 1, 4, 3>(a, st);
+    case 20: return launch_halo<128, 2, 4, 2>(a, st);
+    case 21: return launch_halo<128, 2, 4, 3>(a, st);
     default: return YCX_ERR_UNSUPPORTED;
   }
 }
