@@ -14,6 +14,9 @@
  *                       Detect head 1x1 convs (bias, no act)    nets/detect.py:27-38
  *                       IDetect conv + ImplicitA/M (folded)     nets/idetect.py:26-31
  *   ycx_stem_conv       first Conv on the fp32 NCHW image       nets/common.py:105-106 (Cin=3)
+ *   ycx_stem_conv2      first two Convs fused (3->32, then 3x3   cfg/net/yolov7.yaml:7-8,
+ *                       stride 2 -> 64); the stem output stays   nets/common.py:97-109
+ *                       in LDS
  *   ycx_maxpool         MP / SP / SPPCSPC max-pools             nets/common.py:25-40, 257
  *   ycx_copy_channels   nn.Upsample(None, 2, 'nearest')         cfg/net/yolov7.yaml:71,85
  *                       Concat (only when a slice cannot alias)  nets/common.py:54-60
@@ -33,7 +36,7 @@
 extern "C" {
 #endif
 
-#define YCX_ABI_VERSION 1
+#define YCX_ABI_VERSION 2
 
 typedef int32_t ycx_status;
 enum {
@@ -130,7 +133,7 @@ typedef struct ycx_nms_desc {
 } ycx_nms_desc;
 
 /* A pre-built op for ycx_run_ops (the static execution plan of Model.forward). */
-enum { YCX_OP_CONV = 1, YCX_OP_STEM = 2, YCX_OP_POOL = 3, YCX_OP_COPY = 4 };
+enum { YCX_OP_CONV = 1, YCX_OP_STEM = 2, YCX_OP_POOL = 3, YCX_OP_COPY = 4, YCX_OP_STEM2 = 5 };
 typedef struct ycx_op {
   int32_t kind;
   int32_t pad_;
@@ -138,12 +141,15 @@ typedef struct ycx_op {
     ycx_conv_desc conv;
     ycx_pool_desc pool;
     ycx_copy_desc copy;
+    ycx_conv_desc pair[2];  /* STEM2: [0] the stem, [1] the stride-2 conv it feeds */
   } d;
   const void* in;           /* x                                                    */
-  const void* weight;       /* packed weights (conv/stem)                           */
-  const float* bias;        /* bias (conv/stem)                                     */
+  const void* weight;       /* packed weights (conv/stem; STEM2: the stem's)        */
+  const float* bias;        /* bias (conv/stem; STEM2: the stem's)                  */
   void* out;                /* y                                                    */
   const void* residual;     /* optional residual (conv)                             */
+  const void* weight2;      /* STEM2: the second conv's packed bf16 weights         */
+  const float* bias2;       /* STEM2: the second conv's bias                        */
 } ycx_op;
 
 int ycx_abi_version(void);
@@ -162,6 +168,15 @@ ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const void* w,
  * channel count (in_c_stride = channels of the input tensor). */
 ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, const float* w,
                          const float* bias, void* y, void* stream);
+/* The stem (3x3, stride 1 or 2, pad 1, 3 -> 32, bf16 NHWC result kept in LDS)
+ * followed by a 3x3 / stride-2 / pad-1 conv 32 -> cout (cout_pad 64) that
+ * consumes only it: one kernel, the 32-channel stem map never reaches HBM.
+ * `stem` and `conv` are the two layers' own descriptors (conv->h/w = the stem
+ * output size); conv output as for ycx_conv2d (NHWC bf16, channel slice).
+ * Requires conv->ho % 4 == 0 and conv->wo % 32 == 0. */
+ycx_status ycx_stem_conv2(const ycx_conv_desc* stem, const ycx_conv_desc* conv, const float* x,
+                          const float* w_stem, const float* b_stem, const void* w_conv,
+                          const float* b_conv, void* y, void* stream);
 ycx_status ycx_maxpool(const ycx_pool_desc* d, const void* x, void* y, void* stream);
 ycx_status ycx_copy_channels(const ycx_copy_desc* d, const void* x, void* y, void* stream);
 

@@ -18,7 +18,7 @@ def header_symbols():
 def test_header_declares_the_boundary():
     syms = header_symbols()
     for s in ('ycx_conv2d', 'ycx_stem_conv', 'ycx_maxpool', 'ycx_copy_channels', 'ycx_decode', 'ycx_filter_decoded',
-              'ycx_decode_filter', 'ycx_sort_nms', 'ycx_run_ops', 'ycx_strerror', 'ycx_abi_version'):
+              'ycx_decode_filter', 'ycx_sort_nms', 'ycx_run_ops', 'ycx_strerror', 'ycx_abi_version', 'ycx_stem_conv2'):
         assert s in syms
 
 
@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_metadata_without_gpu():
     from ycx import _lib
-    assert _lib.lib.ycx_abi_version() == 1
+    assert _lib.lib.ycx_abi_version() == 2
     for i, st in enumerate(_lib._STRUCTS):
         assert _lib.lib.ycx_struct_size(i) == ctypes.sizeof(st)
     assert _lib.lib.ycx_struct_size(99) == 0

@@ -200,3 +200,43 @@ def test_stem(device, cin, k, s, dtype, h, w, cout):
     got = yd.cpu().permute(0, 3, 1, 2).double()
     tol = 1e-2 if dtype == L.DT_BF16 else 1e-5
     torch.testing.assert_close(got, ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize('stem_s,cout,act', [(1, 64, L.ACT_SILU), (2, 64, L.ACT_LEAKY), (1, 48, L.ACT_SILU)])
+def test_stem_conv2_fused(device, stem_s, cout, act):
+    """ycx_stem_conv2 = stem (3x3, 3->32) then 3x3/s2 conv, stem map kept in LDS
+    (rounded to bf16 there, as the unfused path stores it)."""
+    g = torch.Generator().manual_seed(5)
+    n, h, w = 2, 32 * stem_s, 64 * stem_s
+    x = torch.rand(n, 3, h, w, generator=g)
+    ws = torch.randn(32, 3, 3, 3, generator=g) * 0.3
+    bs = torch.randn(32, generator=g) * 0.1
+    wc = (torch.randn(cout, 32, 3, 3, generator=g) / 17.0).to(torch.bfloat16)
+    bc = torch.randn(cout, generator=g) * 0.1
+    sh, sw = (h - 1) // stem_s + 1, (w - 1) // stem_s + 1
+    ho, wo = (sh - 1) // 2 + 1, (sw - 1) // 2 + 1
+    out_extra = 8
+    y = torch.zeros(n, ho, wo, cout + out_extra, dtype=torch.bfloat16)
+    ds, dc = L.ConvDesc(), L.ConvDesc()
+    ds.n, ds.h, ds.w, ds.cin, ds.in_c_off, ds.in_c_stride = n, h, w, 3, 0, 3
+    ds.ho, ds.wo, ds.cout, ds.cout_pad, ds.out_c_off, ds.out_c_stride = sh, sw, 32, 32, 0, 32
+    ds.kh = ds.kw = 3
+    ds.stride, ds.pad, ds.act, ds.leaky_slope, ds.dtype, ds.out_layout = stem_s, 1, act, 0.1, L.DT_BF16, L.OUT_NHWC
+    dc.n, dc.h, dc.w, dc.cin, dc.in_c_off, dc.in_c_stride = n, sh, sw, 32, 0, 32
+    dc.ho, dc.wo, dc.cout, dc.cout_pad, dc.out_c_off, dc.out_c_stride = ho, wo, cout, 64, out_extra, cout + out_extra
+    dc.kh = dc.kw = 3
+    dc.stride, dc.pad, dc.act, dc.leaky_slope, dc.dtype, dc.out_layout = 2, 1, L.ACT_SILU, 0.1, L.DT_BF16, L.OUT_NHWC
+    wsp = ws.permute(2, 3, 1, 0).contiguous()                      # [kh][kw][cin][cout_pad] fp32
+    wcp = torch.zeros(64, 3, 3, 32, dtype=torch.bfloat16)
+    wcp[:cout] = wc.permute(0, 2, 3, 1)
+    bcp = torch.zeros(64)
+    bcp[:cout] = bc
+    t = [v.to(device) for v in (x, wsp, bs, wcp, bcp, y)]
+    L.check(L.lib.ycx_stem_conv2(ctypes.byref(ds), ctypes.byref(dc), *[v.data_ptr() for v in t],
+                                 L.stream_handle(device)))
+    torch.cuda.synchronize()
+    mid = _ref_conv(x, ws, bs, stem_s, 1, act).to(torch.bfloat16)    # the stem map as bf16
+    ref = _ref_conv(mid.float(), wc.float(), bc, 2, 1, L.ACT_SILU)
+    got = t[5].cpu()
+    assert torch.all(got[..., :out_extra] == 0)
+    torch.testing.assert_close(got[..., out_extra:].permute(0, 3, 1, 2).double(), ref, rtol=2e-2, atol=2e-2)

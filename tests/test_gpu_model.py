@@ -74,7 +74,10 @@ def test_engine_plan_properties(device):
     eng = m.engine_for((2, 3, 640, 640), device)
     s = eng.summary()
     assert s['kinds'].get('copy', 0) == 0, "every concat input should alias its slice (no copy kernels)"
-    assert s['kinds']['conv'] + s['kinds']['stem'] == 92  # 95 convs minus the 3 folded RepConv 1x1 branches
+    k = s['kinds']
+    # 95 convs minus the 3 folded RepConv 1x1 branches; at 640 the stem and layer 1 run fused (stem2)
+    assert k.get('stem2', 0) == 1 and 'stem' not in k
+    assert k['conv'] + 2 * k['stem2'] == 92
     assert abs(s['gflop_per_image'] - 104.511078400) < 1e-6
 
 

@@ -877,6 +877,169 @@ __global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
   }
 }
 
+// -------------------------------------------------------------------------
+// Stem + stride-2 conv, fused (yolov7's layers 0-1: 3x3 3->32, 3x3/s2 32->64).
+// A 256-thread block owns a 4 x 32 tile of the second conv's output and all
+// its (<= 64) channels:
+//  (0) the fp32 image patch under the tile's 9 x 65 stem pixels (3 x 11 x 67
+//      floats at stem stride 1) is loaded into LDS with coalesced loads, all
+//      in flight at once, and the second conv's weights (all 9 taps of the
+//      wave's 32 channels) are requested into registers;
+//  (1) the stem pixels are computed by MFMA (K = 27 <= 32, one instruction per
+//      16 pixels x 16 channels) from that patch and kept in LDS as bf16, 64 B
+//      per pixel, zero outside the stem map (the second conv's padding); even
+//      and odd stem columns live in separate planes so the B fragments of 16
+//      consecutive output pixels are 16 consecutive slots;
+//  (2) the second conv: one tap = one 32-deep MFMA step, B from the stem tile.
+// The 32-channel stem map (839 MB at bs = 32, 640^2) never touches HBM.
+// -------------------------------------------------------------------------
+constexpr int kS2TH = 4, kS2TW = 32;                       // output tile
+constexpr int kS2R = 2 * kS2TH + 1, kS2C = 2 * kS2TW + 1;  // 9 x 65 stem pixels
+constexpr int kS2Even = (kS2C + 1) / 2, kS2Odd = kS2C / 2;
+
+__device__ __forceinline__ int s2_slot(int r, int c) {
+  return (c & 1) ? kS2R * kS2Even + r * kS2Odd + (c >> 1) : r * kS2Even + (c >> 1);
+}
+
+template <int SS>  // stem stride
+__global__ void __launch_bounds__(256) stem2_fused(ConvArgs sa, ConvArgs ca) {
+  constexpr int NPIX = kS2R * kS2C, NGRP = (NPIX + 15) / 16;
+  constexpr int IR = (kS2R - 1) * SS + 3, IC = (kS2C - 1) * SS + 3;  // image patch rows / cols
+  constexpr int IMG = 3 * IR * IC;                                   // floats
+  constexpr int FM = 2, FN = 4;  // per wave: 32 output channels x 64 pixels (2 rows x 32)
+  constexpr int STEM_BYTES = ((NPIX * 64) + 255) & ~255;
+  __shared__ __attribute__((aligned(1024))) char smem[STEM_BYTES + IMG * 4];
+  float* img = reinterpret_cast<float*>(smem + STEM_BYTES);
+  const int tid = threadIdx.x, lane = tid & 63, lx = lane & 15, kq = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv & 1, wn = wv >> 1;  // 32-channel half, 2-row half
+  const int L = ycx_xcd_remap(blockIdx.x, ca.nwg);
+  const int tx_n = ca.Wo / kS2TW, tpi = (ca.Ho / kS2TH) * tx_n;
+  const int n = L / tpi, ti = L - n * tpi;
+  const int oy0 = (ti / tx_n) * kS2TH, ox0 = (ti % tx_n) * kS2TW;
+  const int sy0 = 2 * oy0 - 1, sx0 = 2 * ox0 - 1;          // stem pixel of tile slot (0, 0)
+  const int iy0 = sy0 * SS - sa.P, ix0 = sx0 * SS - sa.P;   // image pixel of patch (0, 0)
+
+  // (0) weights of the second conv, all taps, this wave's 32 channels: A lane
+  //     (co = 32 wm + 16 i + lx, k = 32 t + 8 kq .. +7)
+  const __bf16* __restrict__ Wc = reinterpret_cast<const __bf16*>(ca.w);  // [Cout_pad][3][3][32]
+  constexpr int kAR = 3;  // taps of weights in flight (the first kAR requested before the stem phase)
+  auto load_a = [&](int t, bf16x8 (&a)[FM]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      a[i] = *reinterpret_cast<const bf16x8*>(Wc + (size_t)(32 * wm + 16 * i + lx) * ca.Ktot + 32 * t + 8 * kq);
+  };
+  bf16x8 aw[kAR][FM];
+#pragma unroll
+  for (int t = 0; t < kAR; ++t) load_a(t, aw[t]);
+  // ... and the image patch (fp32, zero outside the image)
+  {
+    const float* __restrict__ X = reinterpret_cast<const float*>(sa.x);
+    const float* Xn = X + (size_t)(n * sa.in_cs + sa.in_coff) * sa.H * sa.W;
+    constexpr int PER = (IMG + 255) / 256;
+    float v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = u * 256 + tid;
+      const int c = e / (IR * IC), rem = e - c * (IR * IC), r = rem / IC, col = rem - r * IC;
+      const int iy = iy0 + r, ix = ix0 + col;
+      const bool ok = e < IMG && (unsigned)iy < (unsigned)sa.H && (unsigned)ix < (unsigned)sa.W;
+      v[u] = ok ? Xn[(size_t)c * sa.H * sa.W + iy * sa.W + ix] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u)
+      if (u * 256 + tid < IMG) img[u * 256 + tid] = v[u];
+  }
+  __syncthreads();
+
+  // (1) stem tile
+  {
+    constexpr int KT = 27, CIN = 3;
+    const float* Ws = reinterpret_cast<const float*>(sa.w);  // [KT][Cout_pad]
+    bf16x8 af[2];
+    int toff[8];
+    bool kv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * kq + j;
+      kv[j] = k < KT;
+      const int kk = kv[j] ? k : 0, tap = kk / CIN, dc = kk - tap * CIN;
+      const int dy = tap / 3, dx = tap - dy * 3;
+      toff[j] = (dc * IR + dy) * IC + dx;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) af[t][j] = (__bf16)(kv[j] ? Ws[kk * sa.Cout_pad + stem_ch(t, lx)] : 0.0f);
+    }
+    float bias[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[t][r] = sa.bias[stem_ch(t, 4 * kq + r)];
+    // pixel p = 16 g + lx, g = wv, wv + 4, ...: (r, c) advance by 64 pixels per step
+    int pr = (16 * wv + lx) / kS2C, pcc = (16 * wv + lx) - pr * kS2C;
+    for (int g = wv; g < NGRP; g += 4) {
+      const int p = 16 * g + lx;
+      const int r = pr, c = pcc;
+      pcc += 64;
+      if (pcc >= kS2C) { pcc -= kS2C; ++pr; }  // 64 < kS2C: at most one wrap
+      const int sy = sy0 + r, sx = sx0 + c;
+      const bool inside = p < NPIX && (unsigned)sy < (unsigned)sa.Ho && (unsigned)sx < (unsigned)sa.Wo;
+      const float* ip = img + (p < NPIX ? (r * SS) * IC + c * SS : 0);  // tap (0, 0), channel 0
+      bf16x8 b;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = (__bf16)(kv[j] ? ip[toff[j]] : 0.0f);
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], b, z, 0, 0, 0);
+      const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], b, z, 0, 0, 0);
+      bf16x8 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // zero outside the stem map: the second conv's padding
+        o[q] = (__bf16)(inside ? ycx_act<true>(c0[q] + bias[0][q], sa.act, sa.slope) : 0.0f);
+        o[4 + q] = (__bf16)(inside ? ycx_act<true>(c1[q] + bias[1][q], sa.act, sa.slope) : 0.0f);
+      }
+      if (p < NPIX) *reinterpret_cast<bf16x8*>(smem + s2_slot(r, c) * 64 + 16 * kq) = o;
+    }
+  }
+  __syncthreads();
+
+  // (2) second conv: wave (wm, wn) -> channels 32 wm.., output rows 2 wn, 2 wn + 1
+  //     (fragment j: row rr = 2 wn + (j >> 1), cols cc = 16 (j & 1) + lx). Its
+  //     stem pixel for tap (ky, kx) is (2 rr + ky, 2 cc + kx): even kx in the
+  //     even plane at slot (2 rr + ky) E + cc + kx/2, odd kx in the odd plane at
+  //     R E + (2 rr + ky) O + cc — per-lane bases plus per-tap constants.
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const char* be[FN];
+  const char* bo[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int rr = 2 * wn + (j >> 1), cc = 16 * (j & 1) + lx;
+    be[j] = smem + ((2 * rr) * kS2Even + cc) * 64 + 16 * kq;
+    bo[j] = smem + (kS2R * kS2Even + (2 * rr) * kS2Odd + cc) * 64 + 16 * kq;
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int ky = t / 3, kx = t - 3 * ky;
+    bf16x8 bfr[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      bfr[j] = (kx & 1) ? *reinterpret_cast<const bf16x8*>(bo[j] + ky * kS2Odd * 64)
+                        : *reinterpret_cast<const bf16x8*>(be[j] + (ky * kS2Even + kx / 2) * 64);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[t % kAR][i], bfr[j], acc[i][j], 0, 0, 0);
+    if (t + kAR < 9) load_a(t + kAR, aw[t % kAR]);
+  }
+  int pxf[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) pxf[j] = n * ca.HoWo + (oy0 + 2 * wn + (j >> 1)) * ca.Wo + ox0 + 16 * (j & 1);
+  epilogue_frag<FM, FN>(ca, acc, 32 * wm, pxf, lane);
+}
+
 ConvArgs make_args(const ycx_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                    const void* res) {
   ConvArgs a;
@@ -1113,4 +1276,36 @@ extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, cons
   YCX_STEM(6, 6, 3)
 #undef YCX_STEM
   return YCX_ERR_UNSUPPORTED;
+}
+
+extern "C" ycx_status ycx_stem_conv2(const ycx_conv_desc* sd, const ycx_conv_desc* cd, const float* x,
+                                     const float* w_stem, const float* b_stem, const void* w_conv,
+                                     const float* b_conv, void* y, void* stream) {
+  YCX_CHECK_ARG(sd && cd && x && w_stem && b_stem && w_conv && b_conv && y);
+  YCX_CHECK_ARG(sd->n > 0 && sd->h > 0 && sd->w > 0 && cd->n == sd->n);
+  YCX_CHECK_ARG(sd->ho == (sd->h + 2 * sd->pad - sd->kh) / sd->stride + 1);
+  YCX_CHECK_ARG(sd->wo == (sd->w + 2 * sd->pad - sd->kw) / sd->stride + 1);
+  YCX_CHECK_ARG(cd->h == sd->ho && cd->w == sd->wo && cd->cin == sd->cout);
+  YCX_CHECK_ARG(cd->ho == (cd->h + 2 * cd->pad - cd->kh) / cd->stride + 1);
+  YCX_CHECK_ARG(cd->wo == (cd->w + 2 * cd->pad - cd->kw) / cd->stride + 1);
+  YCX_CHECK_ARG(sd->in_c_off >= 0 && sd->in_c_off + sd->cin <= sd->in_c_stride);
+  YCX_CHECK_ARG(cd->cout_pad >= cd->cout && cd->out_c_off >= 0 && cd->out_c_off + cd->cout <= cd->out_c_stride);
+  YCX_CHECK_SUPPORTED(sd->kh == 3 && sd->kw == 3 && sd->pad == 1 && (sd->stride == 1 || sd->stride == 2) &&
+                      sd->cin == 3 && sd->cout == 32 && sd->cout_pad == 32);
+  YCX_CHECK_SUPPORTED(cd->kh == 3 && cd->kw == 3 && cd->stride == 2 && cd->pad == 1 && cd->cin == 32 &&
+                      cd->cout_pad == 64 && cd->cout % 8 == 0 && cd->out_c_off % 8 == 0 && cd->out_c_stride % 8 == 0);
+  YCX_CHECK_SUPPORTED(sd->dtype == YCX_DT_BF16 && cd->dtype == YCX_DT_BF16 && cd->out_layout == YCX_OUT_NHWC);
+  YCX_CHECK_SUPPORTED(sd->act >= YCX_ACT_NONE && sd->act <= YCX_ACT_LEAKY && cd->act >= YCX_ACT_NONE &&
+                      cd->act <= YCX_ACT_LEAKY);
+  YCX_CHECK_SUPPORTED(cd->ho % kS2TH == 0 && cd->wo % kS2TW == 0);
+  YCX_CHECK_SUPPORTED((long long)cd->n * cd->ho * cd->wo < (1LL << 31));
+  ConvArgs sa = make_args(sd, x, w_stem, b_stem, nullptr, nullptr);
+  ConvArgs ca = make_args(cd, nullptr, w_conv, b_conv, y, nullptr);
+  ca.nwg = cd->n * (cd->ho / kS2TH) * (cd->wo / kS2TW);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (sd->stride == 1)
+    hipLaunchKernelGGL((stem2_fused<1>), dim3(ca.nwg), dim3(256), 0, st, sa, ca);
+  else
+    hipLaunchKernelGGL((stem2_fused<2>), dim3(ca.nwg), dim3(256), 0, st, sa, ca);
+  return ycx_launch_status();
 }

@@ -155,6 +155,9 @@ static ycx_status run_one(const ycx_op& op, void* stream) {
       return ycx_maxpool(&op.d.pool, op.in, op.out, stream);
     case YCX_OP_COPY:
       return ycx_copy_channels(&op.d.copy, op.in, op.out, stream);
+    case YCX_OP_STEM2:
+      return ycx_stem_conv2(&op.d.pair[0], &op.d.pair[1], (const float*)op.in, (const float*)op.weight, op.bias,
+                            op.weight2, op.bias2, op.out, stream);
     default:
       return YCX_ERR_BAD_ARG;
   }

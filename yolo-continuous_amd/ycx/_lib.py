@@ -18,12 +18,14 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see above)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("YCX_LIB", os.path.join(_HERE, "libycx_hip.so"))
 
+ABI_VERSION = 2
+
 # ---- enums (ycx.h) ----
 YCX_OK, YCX_ERR_BAD_ARG, YCX_ERR_UNSUPPORTED, YCX_ERR_LAUNCH, YCX_ERR_CAPACITY = 0, 1, 2, 3, 4
 DT_BF16, DT_F32 = 0, 1
 ACT_NONE, ACT_SILU, ACT_LEAKY = 0, 1, 2
 OUT_NHWC, OUT_NCHW_F32, OUT_NHWC_UP2 = 0, 1, 2
-OP_CONV, OP_STEM, OP_POOL, OP_COPY = 1, 2, 3, 4
+OP_CONV, OP_STEM, OP_POOL, OP_COPY, OP_STEM2 = 1, 2, 3, 4, 5
 
 _i32 = ctypes.c_int32
 
@@ -75,13 +77,14 @@ class NmsDesc(ctypes.Structure):
 
 
 class _OpUnion(ctypes.Union):
-    _fields_ = [("conv", ConvDesc), ("pool", PoolDesc), ("copy", CopyDesc)]
+    _fields_ = [("conv", ConvDesc), ("pool", PoolDesc), ("copy", CopyDesc), ("pair", ConvDesc * 2)]
 
 
 class Op(ctypes.Structure):
     _fields_ = [("kind", _i32), ("pad_", _i32), ("d", _OpUnion),
                 ("in_", ctypes.c_void_p), ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p),
-                ("out", ctypes.c_void_p), ("residual", ctypes.c_void_p)]
+                ("out", ctypes.c_void_p), ("residual", ctypes.c_void_p),
+                ("weight2", ctypes.c_void_p), ("bias2", ctypes.c_void_p)]
 
 
 _STRUCTS = [ConvDesc, PoolDesc, CopyDesc, DecodeDesc, Cand, FilterDesc, DecodeFilterDesc, NmsDesc, Op]
@@ -96,6 +99,8 @@ _SIGS = [
     ("ycx_conv_pick_tile", _i32, [ctypes.POINTER(ConvDesc)]),
     ("ycx_conv2d", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP]),
     ("ycx_stem_conv", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP]),
+    ("ycx_stem_conv2", _i32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP,
+                              _VP]),
     ("ycx_maxpool", _i32, [ctypes.POINTER(PoolDesc), _VP, _VP, _VP]),
     ("ycx_copy_channels", _i32, [ctypes.POINTER(CopyDesc), _VP, _VP, _VP]),
     ("ycx_decode", _i32, [ctypes.POINTER(DecodeDesc), _VP, _VP, _VP]),
@@ -130,8 +135,8 @@ def _load():
         fn = getattr(handle, name)
         fn.restype = res
         fn.argtypes = args
-    if handle.ycx_abi_version() != 1:
-        raise ImportError(f"ycx: ABI version mismatch ({handle.ycx_abi_version()} != 1)")
+    if handle.ycx_abi_version() != ABI_VERSION:
+        raise ImportError(f"ycx: ABI version mismatch ({handle.ycx_abi_version()} != {ABI_VERSION})")
     for i, st in enumerate(_STRUCTS):
         got = handle.ycx_struct_size(i)
         if got != ctypes.sizeof(st):

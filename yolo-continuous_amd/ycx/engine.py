@@ -368,14 +368,42 @@ class Engine:
             return 64
         return -(-cout // 128) * 128
 
+    def _stem2_pairs(self):
+        """Stem -> 3x3/s2 conv pairs that run as one ycx_stem_conv2 (the stem
+        map stays in LDS): bf16, the stem's output read by that conv only."""
+        pairs = {}
+        if self.dt != L.DT_BF16:
+            return pairs
+        for nd in self.graph.nodes:
+            if nd.kind != 'stem':
+                continue
+            v, p = nd.out, nd.p
+            if v.role != 'act' or len(v.consumers) != 1 or v.buf is None or v.buf.c != v.c:
+                continue
+            c = v.consumers[0]
+            q = c.p
+            if c.kind != 'conv' or c.inputs[0] is not v or q['residual'] is not None or q['layout'] != L.OUT_NHWC:
+                continue
+            if not (p['k'] == 3 and p['p'] == 1 and p['s'] in (1, 2) and int(p['w'].shape[1]) == 3 and
+                    int(p['w'].shape[0]) == 32 and p['layout'] == L.OUT_NHWC):
+                continue
+            if not (q['k'] == 3 and q['s'] == 2 and q['p'] == 1 and int(q['w'].shape[0]) <= 64 and
+                    int(q['w'].shape[0]) % 8 == 0 and q['ho'] % 4 == 0 and q['wo'] % 32 == 0):
+                continue
+            pairs[id(nd)] = c
+        return pairs
+
     def _build(self):
         dev, dt = self.device, self.dtype
         self.buffers, self.params = [], []
+        pairs = self._stem2_pairs()
+        fused = {id(c) for c in pairs.values()}
+        skip_vals = {id(nd.out) for nd in self.graph.nodes if id(nd) in pairs}  # stem maps that stay in LDS
         seen = set()
         for node in self.graph.nodes:
             for v in [node.out] + node.inputs:
                 b = v.buf
-                if b is not None and id(b) not in seen:
+                if b is not None and id(b) not in seen and id(v) not in skip_vals:
                     seen.add(id(b))
                     b.tensor = torch.empty((b.n, b.h, b.w, b.c), dtype=dt, device=dev)
                     self.buffers.append(b.tensor)
@@ -383,7 +411,11 @@ class Engine:
         self.conv_flops = 0
         for node in self.graph.nodes:
             k = node.kind
-            if k in ('conv', 'stem'):
+            if id(node) in fused:
+                continue
+            if id(node) in pairs:
+                ops.append(self._stem2_op(node, pairs[id(node)]))
+            elif k in ('conv', 'stem'):
                 ops.append(self._conv_op(node))
             elif k == 'pool':
                 ops.append(self._pool_op(node))
@@ -411,7 +443,8 @@ class Engine:
             return None
         return v.buf.tensor.data_ptr()
 
-    def _conv_op(self, node):
+    def _conv_parts(self, node):
+        """Packed weights/bias (kept alive in self.params) and the descriptor of a conv/stem node."""
         p, x, out = node.p, node.inputs[0], node.out
         w64, b64 = p['w'], p['b']
         cout, cin, k = int(w64.shape[0]), int(w64.shape[1]), p['k']
@@ -446,6 +479,14 @@ class Engine:
         if r is not None:
             d.res_c_off, d.res_c_stride = r.coff, r.buf.c
         d.tile = 0
+        flops = 2 * x.n * p['ho'] * p['wo'] * cout * cin * k * k
+        self.conv_flops += flops
+        return d, wt, bt, flops, (x.n, x.h, x.w, cin, cout, k, p['s'])
+
+    def _conv_op(self, node):
+        x, out, r = node.inputs[0], node.out, node.p['residual']
+        stem = node.kind == 'stem'
+        d, wt, bt, flops, shape = self._conv_parts(node)
         op = L.Op()
         op.kind = L.OP_STEM if stem else L.OP_CONV
         op.d.conv = d
@@ -454,12 +495,23 @@ class Engine:
         op.weight, op.bias = wt.data_ptr(), bt.data_ptr()
         op.out = self._val_ptr(out, idx, 'out')
         op.residual = r.buf.tensor.data_ptr() if r is not None else None
-        flops = 2 * x.n * p['ho'] * p['wo'] * cout * cin * k * k
-        self.conv_flops += flops
         tile = 0 if stem else int(L.lib.ycx_conv_pick_tile(ctypes.byref(d)))
         name = 'stem' if stem else L.lib.ycx_conv_tile_name(tile).decode()
-        self.op_info.append(dict(kind=node.kind, name=name, flops=flops,
-                                 shape=(x.n, x.h, x.w, cin, cout, k, p['s'])))
+        self.op_info.append(dict(kind=node.kind, name=name, flops=flops, shape=shape))
+        return op
+
+    def _stem2_op(self, stem, conv):
+        ds, ws, bs, fs, _ = self._conv_parts(stem)
+        dc, wc, bc, fc, shape = self._conv_parts(conv)
+        op = L.Op()
+        op.kind = L.OP_STEM2
+        op.d.pair[0], op.d.pair[1] = ds, dc
+        idx = len(self.op_info)
+        op.in_ = self._val_ptr(stem.inputs[0], idx, 'in_')
+        op.weight, op.bias = ws.data_ptr(), bs.data_ptr()
+        op.weight2, op.bias2 = wc.data_ptr(), bc.data_ptr()
+        op.out = self._val_ptr(conv.out, idx, 'out')
+        self.op_info.append(dict(kind='stem2', name='stem2_fused', flops=fs + fc, shape=shape))
         return op
 
     def _pool_op(self, node):
