@@ -76,8 +76,10 @@ def test_engine_plan_properties(device):
     assert s['kinds'].get('copy', 0) == 0, "every concat input should alias its slice (no copy kernels)"
     k = s['kinds']
     # 95 convs minus the 3 folded RepConv 1x1 branches; at 640 the stem and layer 1 run fused (stem2)
+    # and the 8 ELAN cv1/cv2 sibling pairs run as one conv each
     assert k.get('stem2', 0) == 1 and 'stem' not in k
-    assert k['conv'] + 2 * k['stem2'] == 92
+    assert sum(i.get('parts', 1) for i in eng.op_info if i['kind'] in ('conv', 'stem', 'stem2')) == 92
+    assert sum(1 for i in eng.op_info if i['kind'] == 'conv' and i['parts'] == 2) == 8
     assert abs(s['gflop_per_image'] - 104.511078400) < 1e-6
 
 

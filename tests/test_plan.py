@@ -46,6 +46,7 @@ def test_plan_yolov7_layout():
     plan = Plan(Model(cvt_cfg('yolov7'), ANCHORS, 80), (2, 3, 640, 640))
     c = plan.counts()
     assert c['stem'] == 1 and c['conv'] + c['stem'] == 92  # 95 convs minus the 3 folded RepConv 1x1 branches
+    assert c['merged'] == 8  # ELAN cv1/cv2 sibling 1x1 pairs stacked into one conv each
     assert c['pool'] == 8  # 5 MP (k2s2) + the SPPCSPC 5/9/13 set as a 3-deep k5 cascade
     assert all(nd.p['k'] in (2, 5) for nd in plan.graph.nodes if nd.kind == 'pool')
 

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -295,9 +296,14 @@ class Plan:
                    * nd.p['k'] ** 2 for nd in self.graph.nodes if nd.kind in ('conv', 'stem'))
 
     def counts(self):
+        """Node kinds after the passes; 'conv' counts the original convs (a merged
+        sibling pair counts 2), 'merged' the merged nodes."""
         c = {}
         for nd in self.graph.nodes:
             kind = nd.kind
+            if kind == 'conv' and nd.p.get('parts', 1) > 1:
+                c['merged'] = c.get('merged', 0) + 1
+                c['conv'] = c.get('conv', 0) + nd.p['parts'] - 1
             if kind == 'concat':
                 c['copy'] = c.get('copy', 0) + len(nd.p['copies'])
             c[kind] = c.get(kind, 0) + 1
@@ -342,6 +348,52 @@ class Plan:
             v = node.out
             if v.buf is None and v.role == 'act':
                 v.buf = Buf(v.n, v.h, v.w, v.c)
+        if not os.environ.get("YCX_NO_SIBLING_MERGE"):  # A/B switch for the bench
+            self._merge_sibling_1x1()
+
+    def _merge_sibling_1x1(self):
+        """Two 1x1 convs that read the same activation and write adjacent channel
+        slices of one buffer (ELAN's cv1/cv2 pair feeding its concat, e.g.
+        cfg/net/yolov7.yaml:17-18) become one conv with the weights stacked: the
+        input is read once and the GEMM is twice as wide. Every output channel
+        is the same dot product over the same K as before."""
+        g = self.graph
+
+        def mergeable(nd):
+            p = nd.p
+            return (nd.kind == 'conv' and p['k'] == 1 and p['s'] == 1 and p['p'] == 0 and p['residual'] is None
+                    and p['layout'] == L.OUT_NHWC and nd.out.role == 'act' and nd.out.buf is not None)
+
+        changed = True
+        while changed:
+            changed = False
+            cands = [nd for nd in g.nodes if mergeable(nd)]
+            for a in cands:
+                for b in cands:
+                    if a is b or a.inputs[0] is not b.inputs[0]:
+                        continue
+                    if (a.p['act'], a.p['slope']) != (b.p['act'], b.p['slope']):
+                        continue
+                    va, vb = a.out, b.out
+                    if va.buf is not vb.buf or va.coff + va.c != vb.coff:
+                        continue
+                    out = Val(va.n, va.h, va.w, va.c + vb.c)
+                    out.buf, out.coff = va.buf, va.coff
+                    w = torch.cat([a.p['w'], b.p['w']], 0)
+                    bias = torch.cat([a.p['b'], b.p['b']], 0)
+                    m = Node('conv', [a.inputs[0]], out, **dict(a.p, w=w, b=bias,
+                                                               parts=a.p.get('parts', 1) + b.p.get('parts', 1)))
+                    out.producer = m
+                    va.producer = vb.producer = m  # the halves stay valid views for their consumers
+                    x = a.inputs[0]
+                    x.consumers = [c for c in x.consumers if c is not a and c is not b] + [m]
+                    i = min(g.nodes.index(a), g.nodes.index(b))
+                    g.nodes = [nd for nd in g.nodes if nd is not a and nd is not b]
+                    g.nodes.insert(i, m)
+                    changed = True
+                    break
+                if changed:
+                    break
 
 
 class Engine:
@@ -497,7 +549,7 @@ class Engine:
         op.residual = r.buf.tensor.data_ptr() if r is not None else None
         tile = 0 if stem else int(L.lib.ycx_conv_pick_tile(ctypes.byref(d)))
         name = 'stem' if stem else L.lib.ycx_conv_tile_name(tile).decode()
-        self.op_info.append(dict(kind=node.kind, name=name, flops=flops, shape=shape))
+        self.op_info.append(dict(kind=node.kind, name=name, flops=flops, shape=shape, parts=node.p.get('parts', 1)))
         return op
 
     def _stem2_op(self, stem, conv):
@@ -511,7 +563,7 @@ class Engine:
         op.weight, op.bias = ws.data_ptr(), bs.data_ptr()
         op.weight2, op.bias2 = wc.data_ptr(), bc.data_ptr()
         op.out = self._val_ptr(conv.out, idx, 'out')
-        self.op_info.append(dict(kind='stem2', name='stem2_fused', flops=fs + fc, shape=shape))
+        self.op_info.append(dict(kind='stem2', name='stem2_fused', flops=fs + fc, shape=shape, parts=2))
         return op
 
     def _pool_op(self, node):
