@@ -25,6 +25,9 @@
  *   ycx_decode_filter   decode_box + the same filter, fused     detect.py:29-121
  *   ycx_sort_nms        per-class torchvision.ops.nms loop      detect.py:124-137
  *   ycx_run_ops         Model.forward layer loop                nets/yolo.py:143-153
+ *   ycx_letterbox       image -> network input                   detect.py:16-26,
+ *                                                                image_enhance/letter_box.py:27-60
+ *   ycx_correct_boxes   yolo_correct_boxes on the NMS output     detect.py:139-165
  */
 #ifndef YCX_H_
 #define YCX_H_
@@ -132,6 +135,30 @@ typedef struct ycx_nms_desc {
   double iou_thres;         /* compared as (double)iou > iou_thres, like torchvision */
 } ycx_nms_desc;
 
+/* Letterbox of one uint8 HWC image (BGR kept, as detect.py feeds it) into an
+ * fp32 CHW network input: bilinear resize to new_h x new_w (half-pixel
+ * centres, edge clamp, float64 weights, round-half-even to uint8), content at
+ * (top, left) of out_h x out_w, border value `pad`, then value / 255 in fp32.
+ * The host computes the geometry (round(w r) etc.) like letter_box.py. */
+typedef struct ycx_letterbox_desc {
+  int32_t h0, w0, c;          /* source image (c <= 4)                     */
+  int32_t src_row_stride;     /* bytes between source rows (>= w0 * c)     */
+  int32_t out_h, out_w;       /* letterboxed size                          */
+  int32_t new_h, new_w;       /* resized content size                      */
+  int32_t top, left;          /* content offset                            */
+  int32_t pad;                /* border value, 114 in the reference        */
+} ycx_letterbox_desc;
+
+/* yolo_correct_boxes (detect.py:139-165) applied in place to the padded NMS
+ * output dets[n][max_det][7]: rows 0..min(counts[i], max_det) become
+ * [y1, x1, y2, x2] in original-image pixels (float64 math, stored fp32, as
+ * numpy does). image_hw: [n][2] int32 original (h, w) per image. */
+typedef struct ycx_correct_desc {
+  int32_t n, max_det;
+  int32_t input_h, input_w;   /* network input size                        */
+  int32_t letterbox;          /* letterbox_image flag                      */
+} ycx_correct_desc;
+
 /* A pre-built op for ycx_run_ops (the static execution plan of Model.forward). */
 enum { YCX_OP_CONV = 1, YCX_OP_STEM = 2, YCX_OP_POOL = 3, YCX_OP_COPY = 4, YCX_OP_STEM2 = 5 };
 typedef struct ycx_op {
@@ -155,7 +182,8 @@ typedef struct ycx_op {
 int ycx_abi_version(void);
 /* sizeof() of the ABI structs, so FFI mirrors can verify their layout:
  * 0 conv_desc, 1 pool_desc, 2 copy_desc, 3 decode_desc, 4 cand, 5 filter_desc,
- * 6 decode_filter_desc, 7 nms_desc, 8 op. Returns 0 for an unknown id. */
+ * 6 decode_filter_desc, 7 nms_desc, 8 op, 9 letterbox_desc, 10 correct_desc.
+ * Returns 0 for an unknown id. */
 size_t ycx_struct_size(int32_t which);
 const char* ycx_strerror(ycx_status s);
 const char* ycx_conv_tile_name(int32_t tile);
@@ -199,6 +227,10 @@ size_t ycx_nms_workspace_size(const ycx_nms_desc* d);
 ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, const int32_t* cand_rows,
                         const int32_t* cand_counts, void* workspace, size_t workspace_bytes,
                         float* dets, int32_t* keep_rows, int32_t* keep_counts, void* stream);
+
+ycx_status ycx_letterbox(const ycx_letterbox_desc* d, const uint8_t* src, float* dst, void* stream);
+ycx_status ycx_correct_boxes(const ycx_correct_desc* d, float* dets, const int32_t* counts,
+                             const int32_t* image_hw, void* stream);
 
 /* Run a static op list in order on one stream. If `events` is non-null it must
  * hold n_ops+1 hipEvent_t; event i is recorded before op i and event n_ops

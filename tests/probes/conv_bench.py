@@ -27,6 +27,9 @@ SHAPES = [  # n, h, w, cin, cout, k, s
     (32, 80, 80, 256, 255, 1, 1),
     (32, 80, 80, 128, 256, 3, 1),
     (32, 80, 80, 64, 64, 3, 1),
+    (32, 40, 40, 1024, 1024, 1, 1),
+    (32, 80, 80, 256, 256, 1, 1),
+    (32, 40, 40, 256, 512, 3, 1),
 ]
 
 
@@ -38,7 +41,9 @@ def run(shape, tile, iters=20):
     cpad = 64 if cout <= 64 else -(-cout // 128) * 128
     if tile == 11:
         cpad = -(-cout // 256) * 256
-    if tile in (1, 4, 7, 9, 12, 14, 16, 20, 21) and cpad % 128:
+    if tile in (1, 4, 7, 9, 12, 14, 16, 20, 21, 22, 23) and cpad % 128:
+        return None
+    if tile == 24 and cpad % 256:
         return None
     x = torch.randn(n, h, w, cin, device=dev).to(torch.bfloat16)
     wt = (torch.randn(cpad, k * k * cin, device=dev) * 0.05).to(torch.bfloat16)

@@ -1,0 +1,71 @@
+"""Image-side steps on the GPU:
+ycx_letterbox vs the CPU restatement (bit-exact fp32), ycx_correct_boxes vs the
+reference's numpy yolo_correct_boxes (bit-exact), headless predict()."""
+import numpy as np
+import pytest
+import torch
+import yaml
+
+from helpers import ANCHORS, MASK
+from oracle import ref_letterbox
+from ycx.detect import correct_boxes_device, predict, yolo_correct_boxes
+from ycx.utils.letterbox import letterbox_geometry, letterbox_gpu
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('hw', [(512, 773), (640, 640), (900, 300), (3, 5), (1080, 1920), (480, 640)])
+def test_letterbox_matches_restatement(device, hw):
+    g = np.random.default_rng(hw[0] * 7 + hw[1])
+    img = g.integers(0, 256, size=(*hw, 3), dtype=np.uint8)
+    want = ref_letterbox.letterbox_tensor(img, (640, 640))
+    got = letterbox_gpu(img, (640, 640), device=device).cpu().numpy()
+    assert got.shape == want.shape
+    np.testing.assert_array_equal(got, want)
+    assert letterbox_geometry(*hw) == ref_letterbox.letterbox_geometry(*hw)
+
+
+def test_letterbox_into_batch_slot(device):
+    imgs = [np.full((100, 200, 3), v, dtype=np.uint8) for v in (0, 255)]
+    batch = torch.zeros((2, 3, 320, 320), device=device)
+    for i, im in enumerate(imgs):
+        letterbox_gpu(im, (320, 320), out=batch[i])
+    b = batch.cpu().numpy()
+    for i, im in enumerate(imgs):
+        np.testing.assert_array_equal(b[i], ref_letterbox.letterbox_tensor(im, (320, 320)))
+
+
+@pytest.mark.parametrize('letterbox_image', [True, False])
+@pytest.mark.parametrize('image_hw', [(512, 773), (1080, 1920), (640, 640), (333, 777)])
+def test_correct_boxes_matches_numpy(device, letterbox_image, image_hw):
+    g = np.random.default_rng(sum(image_hw))
+    n, max_det = 3, 50
+    dets = np.zeros((n, max_det, 7), dtype=np.float32)
+    xy = g.random((n, max_det, 2), dtype=np.float32)
+    wh = g.random((n, max_det, 2), dtype=np.float32) * 0.3
+    dets[..., 0:2], dets[..., 2:4] = xy, xy + wh
+    dets[..., 4:7] = g.random((n, max_det, 3), dtype=np.float32)
+    counts = np.array([0, 17, 60], dtype=np.int32)  # empty, partial, more than max_det
+    got = correct_boxes_device(torch.from_numpy(dets).to(device), torch.from_numpy(counts).to(device), (640, 640),
+                               np.array(image_hw), letterbox_image).cpu().numpy()
+    for i in range(n):
+        k = min(int(counts[i]), max_det)
+        o = dets[i, :k].copy()
+        box_xy, box_wh = (o[:, 0:2] + o[:, 2:4]) / 2, o[:, 2:4] - o[:, 0:2]
+        o[:, :4] = yolo_correct_boxes(box_xy, box_wh, (640, 640), np.array(image_hw), letterbox_image)
+        np.testing.assert_array_equal(got[i, :k], o)
+        np.testing.assert_array_equal(got[i, k:], dets[i, k:])  # rows past the count untouched
+
+
+def test_predict_headless(device, tmp_path):
+    plan = dict(device=0, image_size=640, image_chan=3, labels=['raccoon'], model_cfg='yolov7-tiny',
+                anchors=ANCHORS, anchors_mask=MASK)
+    cfg = tmp_path / 'plan.yaml'
+    cfg.write_text(yaml.safe_dump(plan))
+    img = np.random.default_rng(0).integers(0, 256, size=(512, 773, 3), dtype=np.uint8)
+    boxes = predict(str(cfg), image=img, weights='synthetic', device='cuda:0', conf_threshold=0.3,
+                    nms_threshold=0.3)
+    assert isinstance(boxes, list)
+    for b in boxes:  # detect.py:236-244 clamps each corner on one side only, like the reference
+        x1, y1, x2, y2 = b['box']
+        assert x1 >= 0 and y1 >= 0 and x2 <= 773 and y2 <= 512 and b['label'] == 'raccoon'

@@ -81,3 +81,14 @@ def test_nms_restatement_semantics():
     assert ref_post.nms(boxes[[0, 2]], scores[[0, 2]], iou02).tolist() == [0, 1]
     assert ref_post.nms(boxes[[0, 2]], scores[[0, 2]], iou02 - 1e-6).tolist() == [0]
     assert ref_post.nms(boxes[:0], scores[:0], 0.5).numel() == 0
+
+
+def test_letterbox_geometry_restatement():
+    """letter_box.py:27-60 geometry on the SURVEY §8(d) C1 image size (512 x 773 -> 640)."""
+    from oracle import ref_letterbox
+    rw, rh, top, left, oh, ow = ref_letterbox.letterbox_geometry(512, 773, (640, 640))
+    assert (rw, rh, top, left, oh, ow) == (640, 424, 108, 0, 640, 640)
+    img = np.full((512, 773, 3), 7, dtype=np.uint8)
+    t = ref_letterbox.letterbox_tensor(img)
+    assert t.shape == (3, 640, 640) and t.dtype == np.float32
+    assert t[0, 0, 0] == np.float32(114) / np.float32(255) and t[0, 320, 320] == np.float32(7) / np.float32(255)

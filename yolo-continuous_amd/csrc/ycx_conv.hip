@@ -382,17 +382,18 @@ __device__ __forceinline__ void buf_lds16(const void* base, int nbytes, int voff
 // NST = 2 halves the LDS so two workgroups share a CU: one block's prologue
 // and epilogue then overlap the other's MFMA loop (short-K layers).
 template <int BM, int BN, int WM, int WN, bool TT, int NST>
-__global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
-  static_assert(WM * WN == 8, "8 waves");
+__global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
+  constexpr int NW = WM * WN;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(NST == 2 || NST == 3, "pipeline depth");
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int A_PW = BM / 64, B_PW = BN / 64;  // wave-instructions (8 rows each) per wave per stage
+  constexpr int A_PW = BM / (8 * NW), B_PW = BN / (8 * NW);  // wave-instructions (8 rows each) per wave per stage
   constexpr int LPS = A_PW + B_PW;                 // vmcnt per stage per wave
   constexpr int LDS_BYTES = NST * STAGE;           // the epilogue stores straight from registers
-  static_assert(A_PW >= 1 && B_PW >= 1, "tile rows must be multiples of 64");
+  static_assert(A_PW >= 1 && B_PW >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows per wave");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
   const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
@@ -411,13 +412,13 @@ __global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
   int a_off[A_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
-    const int row = 8 * (wid + 8 * i) + lrow;
+    const int row = 8 * (wid + NW * i) + lrow;
     a_off[i] = ((co0 + row) * a.Ktot + ((pch ^ swz<BK>(row)) << 3)) * 2;
   }
   int b_iy0[B_PW], b_ix0[B_PW], b_base[B_PW];
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
-    const int row = 8 * (wid + 8 * i) + lrow;
+    const int row = 8 * (wid + NW * i) + lrow;
     const int p = px0 + row;
     const bool ok = p < a.M;
     const int pp = ok ? p : 0;
@@ -437,7 +438,7 @@ __global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
   auto issue = [&](int s, int buf) {
     char* base = smem + buf * STAGE;
 #pragma unroll
-    for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * (BK * 2), base + (wid + 8 * i) * 1024);
+    for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * (BK * 2), base + (wid + NW * i) * 1024);
     int ky = i_ky, kx = i_kx;
     if (TT) {
       // second tap of the pair; past the last tap it can never pass the bounds test
@@ -451,7 +452,7 @@ __global__ void __launch_bounds__(512) conv_bf16_glds(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < B_PW; ++i) {
       const bool ok = (unsigned)(b_iy0[i] + ky) < (unsigned)a.H && (unsigned)(b_ix0[i] + kx) < (unsigned)a.W;
-      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + A_BYTES + (wid + 8 * i) * 1024);
+      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + A_BYTES + (wid + NW * i) * 1024);
     }
     if (TT) {
       i_tap += 2;
@@ -1114,7 +1115,7 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   a.nsteps = TT ? (a.KH * a.KW + 1) / 2 : a.KH * a.KW * (a.Cin / 64);
   a.n_ct = a.Cout_pad / BM;
   a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST>), dim3(a.nwg), dim3(512), 0, st, a);
+  hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
   return ycx_launch_status();
 }
 

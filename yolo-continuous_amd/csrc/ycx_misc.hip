@@ -224,6 +224,8 @@ extern "C" size_t ycx_struct_size(int32_t which) {
     case 6: return sizeof(ycx_decode_filter_desc);
     case 7: return sizeof(ycx_nms_desc);
     case 8: return sizeof(ycx_op);
+    case 9: return sizeof(ycx_letterbox_desc);
+    case 10: return sizeof(ycx_correct_desc);
     default: return 0;
   }
 }

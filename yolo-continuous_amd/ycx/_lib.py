@@ -87,7 +87,17 @@ class Op(ctypes.Structure):
                 ("weight2", ctypes.c_void_p), ("bias2", ctypes.c_void_p)]
 
 
-_STRUCTS = [ConvDesc, PoolDesc, CopyDesc, DecodeDesc, Cand, FilterDesc, DecodeFilterDesc, NmsDesc, Op]
+class LetterboxDesc(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("h0", "w0", "c", "src_row_stride", "out_h", "out_w", "new_h", "new_w", "top",
+                                    "left", "pad")]
+
+
+class CorrectDesc(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("n", "max_det", "input_h", "input_w", "letterbox")]
+
+
+_STRUCTS = [ConvDesc, PoolDesc, CopyDesc, DecodeDesc, Cand, FilterDesc, DecodeFilterDesc, NmsDesc, Op, LetterboxDesc,
+            CorrectDesc]
 
 # (name, restype, argtypes) — every symbol declared in include/ycx.h.
 _VP = ctypes.c_void_p
@@ -99,6 +109,8 @@ _SIGS = [
     ("ycx_conv_pick_tile", _i32, [ctypes.POINTER(ConvDesc)]),
     ("ycx_conv2d", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP]),
     ("ycx_stem_conv", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP]),
+    ("ycx_letterbox", _i32, [ctypes.POINTER(LetterboxDesc), _VP, _VP, _VP]),
+    ("ycx_correct_boxes", _i32, [ctypes.POINTER(CorrectDesc), _VP, _VP, _VP, _VP]),
     ("ycx_stem_conv2", _i32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP,
                               _VP]),
     ("ycx_maxpool", _i32, [ctypes.POINTER(PoolDesc), _VP, _VP, _VP]),

@@ -108,27 +108,47 @@ def nms_device(prediction, num_classes, conf_thres=0.5, nms_thres=0.4, max_det=N
     return device_nms(cand, cand_rows, counts, num_classes, nms_thres, max_det or rows)
 
 
+def correct_boxes_device(dets, counts, input_shape, image_hw, letterbox_image=True):
+    """yolo_correct_boxes (detect.py:139-165) on the device, in place on the
+    padded NMS output dets [n, max_det, 7]: the kept rows become [y1, x1, y2, x2]
+    in original-image pixels (the numpy float64/float32 arithmetic reproduced
+    exactly). image_hw: one (h, w) for every image, or an [n, 2] array."""
+    _require_device(dets, "dets")
+    n, max_det = dets.shape[0], dets.shape[1]
+    hw = torch.as_tensor(np.asarray(image_hw, dtype=np.int32).reshape(-1, 2))
+    if hw.shape[0] == 1:
+        hw = hw.expand(n, 2)
+    hw = hw.contiguous().to(dets.device)
+    d = L.CorrectDesc()
+    d.n, d.max_det, d.input_h, d.input_w, d.letterbox = n, max_det, int(input_shape[0]), int(input_shape[1]), \
+        int(bool(letterbox_image))
+    L.check(L.lib.ycx_correct_boxes(ctypes.byref(d), dets.data_ptr(), counts.data_ptr(), hw.data_ptr(),
+                                    L.stream_handle(dets.device)), "ycx_correct_boxes")
+    return dets
+
+
 def non_max_suppression(prediction, num_classes, input_shape, image_shape, letterbox_image, conf_thres=0.5,
                         nms_thres=0.4):
     """detect.py:90-144 semantics: list (per image) of np.float32 [K, 7] rows
-    (y1, x1, y2, x2 in original-image pixels, obj, cls_conf, cls) or None."""
+    (y1, x1, y2, x2 in original-image pixels, obj, cls_conf, cls) or None.
+    Everything up to the per-image host lists runs on the device (filter,
+    sort, NMS, yolo_correct_boxes)."""
     dets, _, kc = nms_device(prediction, num_classes, conf_thres, nms_thres)
+    correct_boxes_device(dets, kc, input_shape, image_shape, letterbox_image)
     counts = kc.cpu().numpy()
     dets = dets.cpu().numpy()
     output = [None] * prediction.shape[0]
     for i in range(prediction.shape[0]):
         k = int(counts[i])
-        if k == 0:
-            continue
-        o = dets[i, :k].copy()
-        box_xy, box_wh = (o[:, 0:2] + o[:, 2:4]) / 2, o[:, 2:4] - o[:, 0:2]
-        o[:, :4] = yolo_correct_boxes(box_xy, box_wh, input_shape, image_shape, letterbox_image)
-        output[i] = o
+        if k > 0:
+            output[i] = dets[i, :k].copy()
     return output
 
 
 def yolo_correct_boxes(box_xy, box_wh, input_shape, image_shape, letterbox_image):
-    """Undo the letterbox (numpy, host): returns [y1, x1, y2, x2] in pixels (detect.py:147-165)."""
+    """Undo the letterbox (numpy, host): returns [y1, x1, y2, x2] in pixels
+    (detect.py:147-165). The reference's host helper, kept for its callers;
+    non_max_suppression uses the device form (correct_boxes_device)."""
     box_yx = box_xy[..., ::-1]
     box_hw = box_wh[..., ::-1]
     input_shape = np.array(input_shape)
@@ -299,16 +319,14 @@ def predict(cfg_file, image_path=None, conf_threshold=0.3, nms_threshold=0.3, *,
     from .cfg.train_plan import TrainPlan
     from .utils.helper_io import check_file
     from .utils.helper_torch import select_device
-    from .utils.letterbox import letterbox, read_image
+    from .utils.letterbox import letterbox_gpu, read_image
     plan = TrainPlan(check_file(cfg_file))
     dev = select_device(device if device is not None else plan.device)
     target = (plan.image_size, plan.image_size)
     anchors = np.asarray(plan.anchors).reshape(-1, 2)
     original = image if image is not None else read_image(image_path)
-    data = letterbox(original, target)
-    data = np.expand_dims(np.transpose(data.astype(np.float32) / 255., (2, 0, 1)), 0)
     net = prepare_model(plan, weights=weights, device=dev)
-    images = torch.from_numpy(data).to(dev)
+    images = letterbox_gpu(original, target, device=dev).unsqueeze(0)  # detect.py:23-26 on the GPU
     with torch.no_grad():
         pred = net(images)
     outputs = decode_box(pred, anchors, plan.anchors_mask, plan.num_labels, image_size=target)

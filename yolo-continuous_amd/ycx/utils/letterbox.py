@@ -1,14 +1,20 @@
-"""Host letterbox for predict() (image_enhance/letter_box.py:27-60, scale_fill_prob=0).
+"""Letterbox for predict() (detect.py:16-26, image_enhance/letter_box.py:27-60,
+scale_fill_prob = 0): the geometry on the host, the pixels on the GPU
+(ycx_letterbox: bilinear resize, 114 border, fp32 CHW / 255 in one kernel).
 
-Aspect-preserving resize to round(w*r) x round(h*r) with bilinear sampling
-(cv2.INTER_LINEAR convention: half-pixel centres, edge clamp), then a constant
-114 border split as round(d -/+ 0.1). OpenCV is not installed here, so
-bit-parity with cv2.resize is unpinned; the on-device letterbox
-is the §8(f) "next" row.
+The reference resizes with cv2.resize(INTER_LINEAR); OpenCV is not installed
+here, so the kernel follows the documented INTER_LINEAR convention (half-pixel
+centres, edge clamp) and its bit-parity with cv2 is unpinned;
+tests hold it to the CPU restatement in oracle/ref_letterbox.py.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
+import torch
+
+from .. import _lib as L
 
 
 def read_image(path):
@@ -25,33 +31,36 @@ def read_image(path):
         return np.ascontiguousarray(rgb[..., ::-1])
 
 
-def _resize_bilinear(img, new_w, new_h):
-    h, w = img.shape[:2]
-    sx, sy = w / new_w, h / new_h
-    xs = (np.arange(new_w) + 0.5) * sx - 0.5
-    ys = (np.arange(new_h) + 0.5) * sy - 0.5
-    x0 = np.clip(np.floor(xs).astype(np.int64), 0, w - 1)
-    y0 = np.clip(np.floor(ys).astype(np.int64), 0, h - 1)
-    x1 = np.clip(x0 + 1, 0, w - 1)
-    y1 = np.clip(y0 + 1, 0, h - 1)
-    fx = np.clip(xs - np.floor(xs), 0, 1)[None, :, None]
-    fy = np.clip(ys - np.floor(ys), 0, 1)[:, None, None]
-    f = img.astype(np.float32)
-    top = f[y0][:, x0] * (1 - fx) + f[y0][:, x1] * fx
-    bot = f[y1][:, x0] * (1 - fx) + f[y1][:, x1] * fx
-    return np.clip(np.rint(top * (1 - fy) + bot * fy), 0, 255).astype(np.uint8)
-
-
-def letterbox(img, new_shape=(640, 640), color=(114, 114, 114)):
-    h0, w0 = img.shape[:2]
+def letterbox_geometry(h0, w0, new_shape=(640, 640)):
+    """(rw, rh, top, left, out_h, out_w) as letter_box.py:27-60 computes them."""
     r = min(new_shape[0] / w0, new_shape[1] / h0)
     rw, rh = int(round(w0 * r)), int(round(h0 * r))
     dw, dh = (new_shape[0] - rw) / 2, (new_shape[1] - rh) / 2
-    if (rw, rh) != (w0, h0):
-        img = _resize_bilinear(img, rw, rh)
     top, bottom = int(round(dh - 0.1)), int(round(dh + 0.1))
     left, right = int(round(dw - 0.1)), int(round(dw + 0.1))
-    out = np.empty((rh + top + bottom, rw + left + right, img.shape[2]), dtype=np.uint8)
-    out[...] = np.asarray(color, dtype=np.uint8)
-    out[top:top + rh, left:left + rw] = img
+    return rw, rh, top, left, rh + top + bottom, rw + left + right
+
+
+def letterbox_gpu(image, new_shape=(640, 640), device=None, out=None, pad=114):
+    """HWC uint8 image (numpy or torch) -> letterboxed fp32 CHW tensor on the
+    GPU (BGR kept, values / 255). ``out`` may be a preallocated [C, H, W] fp32
+    device tensor (e.g. one slot of a batch)."""
+    dev = torch.device(device) if device is not None else (out.device if out is not None else torch.device('cuda'))
+    if dev.type != 'cuda':
+        raise RuntimeError("ycx: letterbox_gpu needs a ROCm device; there is no CPU path")
+    src = torch.as_tensor(image)
+    if src.dtype != torch.uint8 or src.dim() != 3:
+        raise ValueError("ycx: letterbox expects an HWC uint8 image")
+    src = src.to(dev).contiguous()
+    h0, w0, c = src.shape
+    rw, rh, top, left, oh, ow = letterbox_geometry(h0, w0, new_shape)
+    if out is None:
+        out = torch.empty((c, oh, ow), dtype=torch.float32, device=dev)
+    if tuple(out.shape) != (c, oh, ow) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError(f"ycx: letterbox output must be a contiguous fp32 [{c}, {oh}, {ow}] tensor")
+    d = L.LetterboxDesc()
+    d.h0, d.w0, d.c, d.src_row_stride = h0, w0, c, w0 * c
+    d.out_h, d.out_w, d.new_h, d.new_w, d.top, d.left, d.pad = oh, ow, rh, rw, top, left, pad
+    L.check(L.lib.ycx_letterbox(ctypes.byref(d), src.data_ptr(), out.data_ptr(), L.stream_handle(dev)),
+            "ycx_letterbox")
     return out
