@@ -23,6 +23,7 @@
  *   ycx_decode          decode_box (one head level)             detect.py:29-87
  *   ycx_filter_decoded  non_max_suppression lines 98-121        detect.py:98-121
  *   ycx_decode_filter   decode_box + the same filter, fused     detect.py:29-121
+ *   ycx_idetect_decode  IDetect eval branch (strides supplied)  nets/idetect.py:33-45
  *   ycx_sort_nms        per-class torchvision.ops.nms loop      detect.py:124-137
  *   ycx_run_ops         Model.forward layer loop                nets/yolo.py:143-153
  *   ycx_letterbox       image -> network input                   detect.py:16-26,
@@ -209,6 +210,14 @@ ycx_status ycx_maxpool(const ycx_pool_desc* d, const void* x, void* y, void* str
 ycx_status ycx_copy_channels(const ycx_copy_desc* d, const void* x, void* y, void* stream);
 
 ycx_status ycx_decode(const ycx_decode_desc* d, const float* head, float* out, void* stream);
+/* IDetect's eval outputs for one level (nets/idetect.py:33-45): xview gets the
+ * raw map as (n, na, h, w, no); z [n][rows_total][no] gets, at row_off, the
+ * decoded rows xy = (sigmoid*2 - 0.5 + grid) * stride, wh = (sigmoid*2)^2 *
+ * anchor (pixels; d->anchors_scaled holds the level's anchor_grid in pixels).
+ * The reference leaves IDetect.stride unset (its eval raises); the caller
+ * supplies it. */
+ycx_status ycx_idetect_decode(const ycx_decode_desc* d, float stride, const float* head, float* z, float* xview,
+                              void* stream);
 /* Candidate outputs of both filters:
  *   cand        [n][rows] ycx_cand, written only at the rows that pass (dense by row)
  *   cand_rows   [n][rows] int32, the passing row indices, compacted (any order)

@@ -138,3 +138,23 @@ def non_max_suppression(prediction, num_classes, input_shape, image_shape, lette
         o[:, :4] = yolo_correct_boxes(box_xy, box_wh, input_shape, image_shape, letterbox_image)
         output.append(o)
     return output
+
+
+def idetect_eval(outs, anchors, na, no, strides):
+    """IDetect's eval branch restated (nets/idetect.py:33-45) on its raw maps
+    (NCHW per level, P3..P5): returns (cat(z, 1), [x_i (bs, na, ny, nx, no)]).
+    The reference never reaches this code (IDetect.stride is None, :8), so the
+    strides are supplied; everything else is its op sequence."""
+    anchor_grid = torch.tensor(anchors).float().view(len(outs), 1, -1, 1, 1, 2)
+    z, xs = [], []
+    for i, xi in enumerate(outs):
+        bs, _, ny, nx = xi.shape
+        xi = xi.view(bs, na, no, ny, nx).permute(0, 1, 3, 4, 2).contiguous()
+        yv, xv = torch.meshgrid([torch.arange(ny), torch.arange(nx)], indexing='ij')
+        grid = torch.stack((xv, yv), 2).view((1, 1, ny, nx, 2)).float()
+        y = xi.sigmoid()
+        y[..., 0:2] = (y[..., 0:2] * 2. - 0.5 + grid) * torch.tensor(strides[i], dtype=torch.float32)
+        y[..., 2:4] = (y[..., 2:4] * 2) ** 2 * anchor_grid[i]
+        z.append(y.view(bs, -1, no))
+        xs.append(xi)
+    return torch.cat(z, 1), xs

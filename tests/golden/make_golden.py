@@ -120,8 +120,37 @@ def run_ref(Model, cfg, nc, x, seed, idetect_raw=False):
     return [t.detach().numpy().copy() for t in ys], sd_hash(sd), len(sd)
 
 
+def make_idetect_eval(Model, manifest):
+    """G4: IDetect's eval branch run by the reference itself. Its stride is
+    None (nets/idetect.py:8) so eval raises; here the strides the build uses
+    (input size / ny) are set on the module first, nothing else is touched."""
+    cfg, nc = mini_nets()['idetect']
+    x = synthetic_images(2, 3, 24, 24, seed=300)
+    m = Model(cfg, ANCHORS, nc).eval()
+    sd = synthetic_state_dict(m, seed=12)
+    m.load_state_dict(sd)
+    strides = [2.0, 4.0, 8.0]  # 24 / (12, 6, 3)
+    m.model[-1].stride = torch.tensor(strides)
+    with torch.no_grad():
+        z, xs = m(x)
+    g4 = {'idetect_eval/z': z.numpy().copy()}
+    for j, t in enumerate(xs):
+        g4[f'idetect_eval/x{j}'] = t.numpy().copy()
+    manifest['g4'] = {'idetect_eval': dict(cfg=cfg, nc=nc, shape=[2, 3, 24, 24], img_seed=300, w_seed=12,
+                                           strides=strides, sd_hash=sd_hash(sd), n_x=len(xs))}
+    np.savez(os.path.join(GOLD, 'g4_idetect.npz'), **g4)
+    print('G4 idetect_eval', z.shape, [t.shape for t in xs])
+
+
 def main():
     Model, detect, cvt_cfg = import_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == 'g4':  # add only the IDetect-eval fixture
+        with open(os.path.join(GOLD, 'manifest.json')) as f:
+            manifest = json.load(f)
+        make_idetect_eval(Model, manifest)
+        with open(os.path.join(GOLD, 'manifest.json'), 'w') as f:
+            json.dump(manifest, f, indent=1)
+        return
     torch.set_num_threads(8)
     os.makedirs(NETDIR, exist_ok=True)
     for name in ('yolov7', 'yolov7-tiny'):
@@ -187,6 +216,7 @@ def main():
                                     n_pass=[int(len(p)) for p in passing], n_keep=[int(len(r)) for r in rows])
         print('G3', name, 'pass', [len(p) for p in passing], 'keep', [len(r) for r in rows])
     np.savez(os.path.join(GOLD, 'g3_post.npz'), **g3)
+    make_idetect_eval(Model, manifest)
     with open(os.path.join(GOLD, 'manifest.json'), 'w') as f:
         json.dump(manifest, f, indent=1)
 

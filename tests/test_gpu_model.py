@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from helpers import ANCHORS, g1_case, make_model, rel_err
-from oracle import ref_forward
+from oracle import ref_forward, ref_post
 from ycx.utils.helper_io import cvt_cfg
 from ycx.utils.synth import synthetic_images
 
@@ -30,14 +30,22 @@ def _outs(y):
 def test_g1_ops(device, manifest, g1, name, precision, tol):
     m, sd, x, e = g1_case(manifest, name, precision)
     m.to(device)
-    outs = _outs(m(x.to(device)))
+    y = m(x.to(device))
+    if name == 'idetect':  # eval branch: (z, [x_i (bs, na, ny, nx, no)]); fixtures hold the x_i
+        z, y = y
+        head = m.model[-1]
+        strides = [x.shape[2] / o.shape[2] for o in y]
+        gold_nchw = [torch.from_numpy(g1[f'{name}/{j}']).permute(0, 1, 4, 2, 3).reshape(o.shape[0], -1, o.shape[2],
+                                                                                       o.shape[3])
+                     for j, o in enumerate(y)]
+        z_ref, _ = ref_post.idetect_eval(gold_nchw, head.anchors.cpu().view(len(y), -1).tolist(), head.na, head.no,
+                                         strides)
+        assert z.shape == z_ref.shape and rel_err(z.cpu(), z_ref) < tol, ('z', rel_err(z.cpu(), z_ref))
+    outs = _outs(y)
     assert len(outs) == e['n_out']
     for j, o in enumerate(outs):
         gold = torch.from_numpy(g1[f'{name}/{j}'])
         o = o.cpu()
-        if name == 'idetect':
-            bs, _, ny, nx = o.shape
-            o = o.view(bs, 3, -1, ny, nx).permute(0, 1, 3, 4, 2)
         assert o.shape == gold.shape
         assert rel_err(o, gold) < tol, (name, j, rel_err(o, gold))
 

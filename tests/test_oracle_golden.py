@@ -92,3 +92,20 @@ def test_letterbox_geometry_restatement():
     t = ref_letterbox.letterbox_tensor(img)
     assert t.shape == (3, 640, 640) and t.dtype == np.float32
     assert t[0, 0, 0] == np.float32(114) / np.float32(255) and t[0, 320, 320] == np.float32(7) / np.float32(255)
+
+
+def test_oracle_idetect_eval(manifest):
+    """IDetect eval (decoded z) vs the reference's own eval output, strides set
+    on its module as the build does (make_golden.make_idetect_eval)."""
+    import os
+    e = manifest['g4']['idetect_eval']
+    g4 = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'g4_idetect.npz'))
+    m, sd = make_model(e['cfg'], e['nc'], e['w_seed'], 'f32')
+    assert sd_hash(sd) == e['sd_hash']
+    x = synthetic_images(*e['shape'], seed=e['img_seed'])
+    outs = ref_forward.build(e['cfg'], ANCHORS, e['nc'], sd)(x)
+    z, xs = ref_post.idetect_eval(outs, ANCHORS, 3, e['nc'] + 5, e['strides'])
+    _close(z.numpy(), g4['idetect_eval/z'])
+    assert len(xs) == e['n_x']
+    for j, t in enumerate(xs):
+        _close(t.numpy(), g4[f'idetect_eval/x{j}'])

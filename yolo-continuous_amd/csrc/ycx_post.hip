@@ -73,6 +73,55 @@ __global__ void __launch_bounds__(256) decode_kernel(ycx_decode_desc d, const fl
   for (int idx = threadIdx.x; idx < ncell * d.no; idx += blockDim.x) ob[idx] = tile[idx];
 }
 
+// ---------------------------------------------------------------------------
+// IDetect eval branch for one level (nets/idetect.py:33-43, with the strides
+// the reference leaves unset supplied by the caller): the raw map re-laid as
+// (bs, na, ny, nx, no) and the decoded rows z (pixel units):
+//   xy = (sigmoid * 2 - 0.5 + grid) * stride,  wh = (sigmoid * 2)^2 * anchor_grid
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) idetect_kernel(ycx_decode_desc d, float stride, const float* __restrict__ head,
+                                                      float* __restrict__ z, float* __restrict__ xview) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];  // [kDecCells][2 * no]
+  const int n = blockIdx.z, a = blockIdx.y;
+  const int hw = d.h * d.w;
+  const int cell0 = blockIdx.x * kDecCells;
+  const int ncell = min(kDecCells, hw - cell0);
+  const float aw = d.anchors_scaled[2 * a], ah = d.anchors_scaled[2 * a + 1];
+  const float* hb = head + ((size_t)n * d.na * d.no + (size_t)a * d.no) * hw;
+  float* raw = tile + kDecCells * d.no;
+  for (int idx = threadIdx.x; idx < d.no * kDecCells; idx += blockDim.x) {
+    const int o = idx / kDecCells, c = idx - o * kDecCells;
+    if (c >= ncell) continue;
+    const int cell = cell0 + c;
+    const float r = hb[(size_t)o * hw + cell];
+    const float p = sigmoidf_ref(r);
+    float v;
+    if (o == 0) {
+      v = ((p * 2.0f) - 0.5f + (float)(cell % d.w)) * stride;
+    } else if (o == 1) {
+      v = ((p * 2.0f) - 0.5f + (float)(cell / d.w)) * stride;
+    } else if (o == 2) {
+      const float t = p * 2.0f;
+      v = (t * t) * aw;
+    } else if (o == 3) {
+      const float t = p * 2.0f;
+      v = (t * t) * ah;
+    } else {
+      v = p;
+    }
+    tile[c * d.no + o] = v;
+    raw[c * d.no + o] = r;
+  }
+  __syncthreads();
+  const size_t row0 = (size_t)a * hw + cell0;  // (a, y, x) order = view(bs, -1, no) of (bs, na, ny, nx, no)
+  float* zb = z + ((size_t)n * d.rows_total + d.row_off + row0) * d.no;
+  float* xb = xview + ((size_t)n * d.na * hw + row0) * d.no;
+  for (int idx = threadIdx.x; idx < ncell * d.no; idx += blockDim.x) {
+    zb[idx] = tile[idx];
+    xb[idx] = raw[idx];
+  }
+}
+
 // Class max with torch.max(dim) semantics (first index of the maximum).
 __device__ __forceinline__ void class_max(const float* row_cls, int nc, int stride, float& best, int& bi) {
   best = row_cls[0];
@@ -180,6 +229,19 @@ extern "C" ycx_status ycx_decode(const ycx_decode_desc* d, const float* head, fl
   const size_t lds = (size_t)kDecCells * d->no * sizeof(float);
   dim3 grid(ycx_cdiv((long long)d->h * d->w, kDecCells), d->na, d->n);
   hipLaunchKernelGGL(decode_kernel, grid, dim3(256), lds, reinterpret_cast<hipStream_t>(stream), *d, head, out);
+  return ycx_launch_status();
+}
+
+extern "C" ycx_status ycx_idetect_decode(const ycx_decode_desc* d, float stride, const float* head, float* z,
+                                         float* xview, void* stream) {
+  YCX_CHECK_ARG(d && head && z && xview);
+  YCX_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->na > 0 && d->no > 5);
+  YCX_CHECK_ARG(d->row_off >= 0 && d->row_off + d->na * d->h * d->w <= d->rows_total);
+  YCX_CHECK_SUPPORTED(d->na <= 8 && d->no <= 256);
+  const size_t lds = (size_t)2 * kDecCells * d->no * sizeof(float);
+  dim3 grid(ycx_cdiv((long long)d->h * d->w, kDecCells), d->na, d->n);
+  hipLaunchKernelGGL(idetect_kernel, grid, dim3(256), lds, reinterpret_cast<hipStream_t>(stream), *d, stride, head, z,
+                     xview);
   return ycx_launch_status();
 }
 

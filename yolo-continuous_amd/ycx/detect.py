@@ -167,6 +167,35 @@ def yolo_correct_boxes(box_xy, box_wh, input_shape, image_shape, letterbox_image
     return boxes
 
 
+def idetect_outputs(head, outs, input_hw):
+    """IDetect's eval return value (nets/idetect.py:33-45) from the engine's raw
+    head maps (NCHW fp32, one per level, P3..P5 order): (z [n, sum na*ny*nx, no]
+    decoded in pixels, [x_i (n, na, ny, nx, no)]), one ycx_idetect_decode per
+    level. The reference leaves IDetect.stride unset (its eval raises
+    TypeError); unless head.stride is given, stride_i = input height / ny_i
+    (documented deviation)."""
+    n, na, no = outs[0].shape[0], head.na, head.no
+    dev = outs[0].device
+    rows = sum(na * o.shape[2] * o.shape[3] for o in outs)
+    z = torch.empty((n, rows, no), dtype=torch.float32, device=dev)
+    xs, off = [], 0
+    grid_anchors = head.anchor_grid.detach().to('cpu', torch.float32).reshape(len(outs), na, 2)
+    st = L.stream_handle(dev)
+    for i, o in enumerate(outs):
+        ny, nx = int(o.shape[2]), int(o.shape[3])
+        stride = float(head.stride[i]) if head.stride is not None else float(np.float32(input_hw[0]) / np.float32(ny))
+        d = L.DecodeDesc()
+        d.n, d.h, d.w, d.na, d.no, d.rows_total, d.row_off = n, ny, nx, na, no, rows, off
+        for a in range(na):
+            d.anchors_scaled[2 * a], d.anchors_scaled[2 * a + 1] = float(grid_anchors[i, a, 0]), float(grid_anchors[i, a, 1])
+        xv = torch.empty((n, na, ny, nx, no), dtype=torch.float32, device=dev)
+        L.check(L.lib.ycx_idetect_decode(ctypes.byref(d), ctypes.c_float(stride), o.contiguous().data_ptr(),
+                                         z.data_ptr(), xv.data_ptr(), st), "ycx_idetect_decode")
+        xs.append(xv)
+        off += na * ny * nx
+    return z, xs
+
+
 class Detector:
     """Fused device pipeline for a fixed batch shape: Model forward (static plan,
     optionally one HIP graph) -> ycx_decode_filter -> ycx_sort_nms.

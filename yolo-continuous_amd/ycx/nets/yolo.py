@@ -187,7 +187,12 @@ class Model(nn.Module):
         if self.training:
             raise RuntimeError("ycx: Model is inference-only on the HIP path (training is out of scope); "
                                "call .eval() first")
-        return self.engine_for(x.shape, x.device).run(x)
+        outs = self.engine_for(x.shape, x.device).run(x)
+        head = self.model[-1]
+        if isinstance(head, IDetect):  # eval branch: (z, x) as nets/idetect.py:45
+            from ..detect import idetect_outputs
+            return idetect_outputs(head, outs, x.shape[2:])
+        return outs
 
     # ---- engine management --------------------------------------------
     def set_precision(self, precision):
