@@ -188,6 +188,8 @@ int ycx_abi_version(void);
 size_t ycx_struct_size(int32_t which);
 const char* ycx_strerror(ycx_status s);
 const char* ycx_conv_tile_name(int32_t tile);
+/* The tile ycx_conv2d uses for d->tile == 0. d->res_c_stride > 0 means the
+ * call will pass a residual (tile 22, the weight-resident 1x1, takes none). */
 int32_t ycx_conv_pick_tile(const ycx_conv_desc* d);
 
 ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const void* w,

@@ -62,6 +62,14 @@ def test_tile_picker():
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 5
     d.cin, d.cout_pad, d.ho, d.wo = 512, 512, 20, 20
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 16
+    d.h = d.w = d.ho = d.wo = 160
+    d.cin, d.cout_pad, d.kh, d.kw, d.stride, d.pad = 256, 256, 1, 1, 1, 0
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 22  # weight-resident pointwise
+    d.res_c_stride = 256
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 16  # ... which stores no residual
+    d.res_c_stride = 0
+    d.cout_pad, d.h, d.w, d.ho, d.wo = 512, 40, 40, 40, 40
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 16  # too few tiles per persistent block
     d.dtype = _lib.DT_F32
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 8
 

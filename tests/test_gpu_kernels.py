@@ -94,6 +94,24 @@ def test_conv_halo3x3(device, tile, cin, cout, hw):
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize('cin', [64, 128, 256, 512])
+@pytest.mark.parametrize('cout', [64, 128, 248, 256, 512])
+def test_conv1x1_wres(device, cin, cout):
+    """Weight-resident 1x1 kernel (tile 22): ragged pixel tail, more ranges than
+    tiles, channel-sliced input/output, cout < cout_pad."""
+    got, ref = _run_conv(device, 2, 13, 11, cin, cout, 1, 1, L.ACT_SILU, 22, L.DT_BF16, in_extra=8, out_extra=16)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize('n,hw,cin,cout', [(2, 128, 256, 256), (1, 128, 256, 512), (4, 128, 128, 128),
+                                           (2, 96, 64, 64), (3, 72, 512, 256)])
+def test_conv1x1_wres_multi_tile(device, n, hw, cin, cout):
+    """Several tiles per persistent block: the LDS ring wraps across tile
+    boundaries with the epilogue stores counted into the next waits."""
+    got, ref = _run_conv(device, n, hw, hw, cin, cout, 1, 1, L.ACT_LEAKY, 22, L.DT_BF16, in_extra=8, out_extra=8)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+
+
 def test_conv_halo3x3_residual_up2(device):
     got, ref = _run_conv(device, 1, 32, 16, 64, 64, 3, 1, L.ACT_LEAKY, 19, L.DT_BF16, residual=True)
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=2e-2)

@@ -21,9 +21,9 @@ import glob
 import json
 import os
 
-OURS = ("conv_bf16_glds", "conv_bf16_kernel", "conv_f32_kernel", "stem_mfma", "stem_kernel", "maxpool_kernel",
-        "copy_kernel", "decode_filter_kernel", "decode_kernel", "filter_decoded_kernel", "nms_prep", "nms_mask",
-        "nms_finish")
+OURS = ("conv_bf16_glds", "conv3x3_halo", "conv_bf16_kernel", "conv_f32_kernel", "stem2_fused", "stem_mfma",
+        "stem_kernel", "maxpool_kernel", "copy_kernel", "decode_filter_kernel", "decode_kernel", "idetect_kernel",
+        "filter_decoded_kernel", "nms_prep", "nms_big", "nms_finish", "letterbox_kernel", "correct_boxes_kernel")
 KIB = 1024
 
 

@@ -1041,6 +1041,158 @@ __global__ void __launch_bounds__(256) stem2_fused(ConvArgs sa, ConvArgs ca) {
   epilogue_frag<FM, FN>(ca, acc, 32 * wm, pxf, lane);
 }
 
+// -------------------------------------------------------------------------
+// 1x1 conv with the weights resident in registers (memory-bound pointwise
+// layers: K = Cin <= 512). A block of WCO x WPX waves is persistent over a
+// contiguous range of PT-pixel tiles; wave (wc, wp) owns output channels
+// 32 wc .. +31 of the block's channel group and pixels TPW wp .. +TPW-1 of
+// every tile, and holds those 32 rows of W (K/4 VGPRs) for the whole launch.
+// Activations stream HBM -> LDS once per tile through an NS-stage LDS-DMA
+// ring; a stage (one barrier step) is SUB 64-channel slabs of PT rows x 128 B,
+// each XOR-swizzled as in conv_bf16_glds, read by all the block's waves. The
+// MFMA A operand never touches LDS, and no block re-reads weight tiles (the
+// im2col kernels pull every weight tile into LDS once per block: for
+// 256 x 256 at 160^2 that doubles the bytes moved into LDS). The ring runs
+// across tile boundaries: a full tile's epilogue issues exactly FM x FN
+// bf16x4 stores per wave and those enter the following counted vmcnt waits
+// (loads, stores and LDS-DMA retire in issue order on gfx950), so the
+// epilogue never drains the ring.
+// Requires 1x1/s1/p0, Cin = 64 KC, NHWC bf16 output without residual.
+// -------------------------------------------------------------------------
+
+// s_waitcnt vmcnt(BASE + nb) lgkmcnt(0) for a uniform runtime nb in [LO, HI]
+// (the count is an immediate: binary search over the encodable values; a
+// count above 63 waits for 63, i.e. for more than needed, which is safe).
+template <int BASE, int LO, int HI>
+__device__ __forceinline__ void wait_vm_counted(int nb) {
+  if constexpr (LO >= HI || BASE + LO >= 63) {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(BASE + LO < 63 ? BASE + LO : 63) : "memory");
+  } else {
+    constexpr int MID = (LO + HI) / 2;
+    if (nb > MID) wait_vm_counted<BASE, MID + 1, HI>(nb);
+    else wait_vm_counted<BASE, LO, MID>(nb);
+  }
+}
+
+template <int WCO, int WPX, int TPW, int KC, int NS, int SUB>
+__global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
+  constexpr int NW = WCO * WPX, PT = TPW * WPX, FM = 2, FN = TPW / 16, BCO = WCO * 32;
+  constexpr int KS = KC / SUB, SLAB = PT * 128, STAGE = SUB * SLAB, A_PW = PT / (8 * NW);
+  constexpr int NSTO = FM * FN;  // bf16x4 stores per wave per tile
+  constexpr int VM_RING = A_PW * SUB * (NS - 2);
+  static_assert(KC % SUB == 0, "slabs per stage");
+  static_assert(A_PW >= 1 && PT % (8 * NW) == 0 && TPW % 16 == 0, "tile rows per wave");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wc = wid % WCO, wp = wid / WCO;
+  const int G = a.n_ct;
+  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
+  const int g = L % G, r = L / G, R = a.nwg / G;
+  const int T = (a.M + PT - 1) / PT;
+  const int t0 = (int)((long long)r * T / R), t1 = (int)((long long)(r + 1) * T / R);
+  if (t0 >= t1) return;  // whole block: no barrier is left waiting
+  const int cob = g * BCO + wc * 32;
+
+  // this wave's weights (A fragments: co = cob + 16 i + (lane & 15), k = 32 kq + 8 (lane >> 4) ..)
+  const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
+  bf16x8 af[2 * KC][FM];
+#pragma unroll
+  for (int kq = 0; kq < 2 * KC; ++kq)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      af[kq][i] = *reinterpret_cast<const bf16x8*>(Wt + (size_t)(cob + 16 * i + (lane & 15)) * a.Ktot + 32 * kq +
+                                                   8 * (lane >> 4));
+  f32x4 bv[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int co = cob + 16 * i + 4 * (lane >> 4);
+    bv[i] = co < a.Cout ? *reinterpret_cast<const f32x4*>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // LDS-DMA: wave-instruction (wid + NW i) fills rows 8 (wid + NW i) .. +7 of a slab
+  const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
+  const int x_bytes = a.M * a.in_cs * 2;
+  const int lrow = lane >> 3, pch = lane & 7;
+  int rrow[A_PW], roff[A_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    rrow[i] = 8 * (wid + NW * i) + lrow;
+    roff[i] = (rrow[i] * a.in_cs + a.in_coff + ((pch ^ swz<64>(rrow[i])) << 3)) * 2;
+  }
+  const int nst = (t1 - t0) * KS;
+  auto issue = [&](int s) {
+    const int tl = s / KS, ks = s - tl * KS;
+    const int px0 = (t0 + tl) * PT;
+    char* base = smem + (s % NS) * STAGE;
+#pragma unroll
+    for (int sb = 0; sb < SUB; ++sb)
+#pragma unroll
+      for (int i = 0; i < A_PW; ++i) {
+        const int off = px0 + rrow[i] < a.M ? px0 * a.in_cs * 2 + roff[i] + (ks * SUB + sb) * 128 : 0x7FFFFFF0;
+        buf_lds16(X, x_bytes, off, 0, base + sb * SLAB + (wid + NW * i) * 1024);
+      }
+  };
+  for (int s = 0; s < NS - 1 && s < nst; ++s) issue(s);
+
+  const bool exact = a.Cout == a.Cout_pad;  // then every full tile stores exactly NSTO times per wave
+  __bf16* __restrict__ Y = reinterpret_cast<__bf16*>(a.y) + a.out_coff;
+  int t = 0;
+  for (int tl = 0; tl < t1 - t0; ++tl) {
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks, ++t) {
+      // wait for stage t: younger than its loads are the NS-2 later stages and
+      // the store batches of the tiles that ended in steps t-NS+1 .. t-1
+      if (t + NS - 2 >= nst) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      } else {
+        const int lo = t - NS + 1 > 0 ? t - NS + 1 : 0;  // tile ends: steps i KS + KS - 1
+        const int nb = exact && t >= KS ? (t - 1 - (KS - 1)) / KS - (lo + KS - 1 - (KS - 1)) / KS + 1 : 0;
+        wait_vm_counted<VM_RING, 0, (NS + KS - 2) / KS * NSTO>(nb * NSTO);
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + NS - 1 < nst) issue(t + NS - 1);
+      const char* B = smem + (t % NS) * STAGE;
+#pragma unroll
+      for (int kk = 0; kk < 2 * SUB; ++kk) {
+        const int c = (kk & 1) * 4 + (lane >> 4);
+        const char* Bs = B + (kk >> 1) * SLAB;
+        bf16x8 bfr[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = wp * TPW + j * 16 + (lane & 15);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * 128 + ((c ^ swz<64>(row)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2 * SUB * ks + kk][i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // epilogue from registers: no global loads here (one would make the compiler drain vmcnt)
+    const int pb = (t0 + tl) * PT + wp * TPW + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int co = cob + 16 * i + 4 * (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        bf16x4 ov;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ov[q] = (__bf16)ycx_act<true>(acc[i][j][q] + bv[i][q], a.act, a.slope);
+        const int p = pb + 16 * j;
+        if (p < a.M && co < a.Cout) *reinterpret_cast<bf16x4*>(Y + (size_t)p * a.out_cs + co) = ov;
+      }
+    }
+  }
+}
+
 ConvArgs make_args(const ycx_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                    const void* res) {
   ConvArgs a;
@@ -1084,6 +1236,7 @@ const TileInfo kTiles[] = {
     {64, 256, 64, "halo3x3_co64_t16x16"},
     {128, 256, 64, "halo3x3_co128_t16x16_s2"},
     {128, 256, 64, "halo3x3_co128_t16x16_s3"},
+    {32, 64, 64, "wres1x1"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -1119,6 +1272,41 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
+
+// Weight-resident 1x1 (tile 22): the wave split follows cout_pad, the K unroll Cin.
+template <int WCO, int WPX, int TPW, int NS, int SUB>
+ycx_status launch_wres_k(ConvArgs a, hipStream_t st) {
+  a.n_ct = a.Cout_pad / (WCO * 32);
+  const int T = (a.M + TPW * WPX - 1) / (TPW * WPX);
+  const int R = std::max(1, std::min(T, 256 / a.n_ct));
+  a.nwg = R * a.n_ct;
+  dim3 g(a.nwg), b(WCO * WPX * 64);
+  switch (a.Cin) {
+    case 64: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 1, NS, 1>), g, b, 0, st, a); break;
+    case 128: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 2, NS, SUB>), g, b, 0, st, a); break;
+    case 256: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 4, NS, SUB>), g, b, 0, st, a); break;
+    case 512: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 8, NS, SUB>), g, b, 0, st, a); break;
+    default: return YCX_ERR_UNSUPPORTED;
+  }
+  return ycx_launch_status();
+}
+
+bool wres_ok(const ConvArgs& a) {
+  return a.KH == 1 && a.KW == 1 && a.S == 1 && a.P == 0 && a.H == a.Ho && a.W == a.Wo && !a.res &&
+         a.out_layout == YCX_OUT_NHWC && (a.Cin == 64 || a.Cin == 128 || a.Cin == 256 || a.Cin == 512) &&
+         (a.Cout_pad == 64 || a.Cout_pad == 128 || a.Cout_pad % 256 == 0) &&
+         (long long)a.M * a.in_cs * 2 < (1LL << 31) - 64;
+}
+
+// tests/probes/conv_bench.py (bs 32): 160^2 256->256 0.30 -> 0.22 ms, 80^2 512->512 0.24 -> 0.16 ms,
+// 160^2 256->128 0.17 -> 0.13 ms against tile 16
+ycx_status launch_wres(ConvArgs a, hipStream_t st) {
+  if (!wres_ok(a)) return YCX_ERR_UNSUPPORTED;
+  if (a.Cout_pad % 256 == 0) return launch_wres_k<8, 1, 64, 5, 2>(a, st);  // 16 KB stages
+  if (a.Cout_pad == 128) return launch_wres_k<4, 2, 64, 6, 1>(a, st);
+  return launch_wres_k<2, 4, 32, 6, 1>(a, st);
+}
+
 }  // namespace
 
 extern "C" const char* ycx_conv_tile_name(int32_t tile) {
@@ -1128,8 +1316,7 @@ extern "C" const char* ycx_conv_tile_name(int32_t tile) {
 
 // Tile heuristic: pick the largest tile that still gives >= ~2 waves of blocks
 // on 256 CUs, with BK = 32 only where cin is not a multiple of 64.
-extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {
-  if (!d) return 0;
+static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {
   if (d->dtype == YCX_DT_F32) return 8;
   const long long M = (long long)d->n * d->ho * d->wo;
   const bool k64 = (d->cin % 64) == 0;
@@ -1148,6 +1335,14 @@ extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {
     return 5;
   }
   if (!fits) return d->cout_pad % 128 == 0 ? 1 : 2;
+  // Pointwise layers with K <= 512 and >= 8 pixel tiles per persistent block:
+  // weights resident in registers (tile 22; the 160^2 / 80^2 yolov7 1x1s)
+  if (allow_wres && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 &&
+      d->out_layout == YCX_OUT_NHWC && d->cin <= 512 && (d->cin & (d->cin - 1)) == 0 &&
+      (d->cout_pad == 64 || d->cout_pad == 128 || d->cout_pad % 256 == 0)) {
+    const long long pt = d->cout_pad >= 256 ? 64 : 128, groups = d->cout_pad >= 256 ? d->cout_pad / 256 : 1;
+    if (M >= 8 * pt * (256 / groups)) return 22;
+  }
   // 3x3 stride-1 'same' convs on 16-aligned maps: LDS halo tiles (tests/probes/conv_bench.py:
   // +14-18 % over the im2col tiles at 80^2 with >= 128 output channels, +18 % at 320^2 x 64)
   if (d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->h == d->ho && d->w == d->wo &&
@@ -1162,6 +1357,11 @@ extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {
   if ((M + 255) / 256 >= 2048) return 15;
   if ((d->cout_pad / 64) * ((M + 127) / 128) >= 256) return 18;
   return 3;
+}
+
+extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {
+  if (!d) return 0;
+  return pick_tile(d, d->res_c_stride == 0);  // res_c_stride > 0: the call will pass a residual
 }
 
 extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const void* w, const float* bias,
@@ -1189,7 +1389,7 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ConvArgs a = make_args(d, x, w, bias, y, residual);
 
-  int tile = d->tile ? d->tile : ycx_conv_pick_tile(d);
+  int tile = d->tile ? d->tile : pick_tile(d, residual == nullptr);  // tile 22 stores no residual
   YCX_CHECK_SUPPORTED(tile > 0 && tile < kNumTiles);
   const TileInfo& t = kTiles[tile];
   YCX_CHECK_SUPPORTED(d->cin % t.bk == 0 && d->cout_pad % t.bm == 0);
@@ -1222,6 +1422,7 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
     case 19: return launch_halo<64, 1, 4, 3>(a, st);
     case 20: return launch_halo<128, 2, 4, 2>(a, st);
     case 21: return launch_halo<128, 2, 4, 3>(a, st);
+    case 22: return launch_wres(a, st);
     default: return YCX_ERR_UNSUPPORTED;
   }
 }
