@@ -220,7 +220,8 @@ def test_stem(device, cin, k, s, dtype, h, w, cout):
     torch.testing.assert_close(got, ref, rtol=tol, atol=tol)
 
 
-@pytest.mark.parametrize('stem_s,cout,act', [(1, 64, L.ACT_SILU), (2, 64, L.ACT_LEAKY), (1, 48, L.ACT_SILU)])
+@pytest.mark.parametrize('stem_s,cout,act', [(1, 64, L.ACT_SILU), (2, 64, L.ACT_LEAKY), (1, 48, L.ACT_SILU),
+                                             (1, 64, L.ACT_NONE), (2, 32, L.ACT_SILU)])
 def test_stem_conv2_fused(device, stem_s, cout, act):
     """ycx_stem_conv2 = stem (3x3, 3->32) then 3x3/s2 conv, stem map kept in LDS
     (rounded to bf16 there, as the unfused path stores it)."""
@@ -243,7 +244,7 @@ def test_stem_conv2_fused(device, stem_s, cout, act):
     dc.n, dc.h, dc.w, dc.cin, dc.in_c_off, dc.in_c_stride = n, sh, sw, 32, 0, 32
     dc.ho, dc.wo, dc.cout, dc.cout_pad, dc.out_c_off, dc.out_c_stride = ho, wo, cout, 64, out_extra, cout + out_extra
     dc.kh = dc.kw = 3
-    dc.stride, dc.pad, dc.act, dc.leaky_slope, dc.dtype, dc.out_layout = 2, 1, L.ACT_SILU, 0.1, L.DT_BF16, L.OUT_NHWC
+    dc.stride, dc.pad, dc.act, dc.leaky_slope, dc.dtype, dc.out_layout = 2, 1, act, 0.1, L.DT_BF16, L.OUT_NHWC
     wsp = ws.permute(2, 3, 1, 0).contiguous()                      # [kh][kw][cin][cout_pad] fp32
     wcp = torch.zeros(64, 3, 3, 32, dtype=torch.bfloat16)
     wcp[:cout] = wc.permute(0, 2, 3, 1)
@@ -254,7 +255,7 @@ def test_stem_conv2_fused(device, stem_s, cout, act):
                                  L.stream_handle(device)))
     torch.cuda.synchronize()
     mid = _ref_conv(x, ws, bs, stem_s, 1, act).to(torch.bfloat16)    # the stem map as bf16
-    ref = _ref_conv(mid.float(), wc.float(), bc, 2, 1, L.ACT_SILU)
+    ref = _ref_conv(mid.float(), wc.float(), bc, 2, 1, act)
     got = t[5].cpu()
     assert torch.all(got[..., :out_extra] == 0)
     torch.testing.assert_close(got[..., out_extra:].permute(0, 3, 1, 2).double(), ref, rtol=2e-2, atol=2e-2)

@@ -23,6 +23,7 @@
 // fp32 FMA chain), used to prove the 1e-3 relative bound vs the fp32 CPU
 // reference.
 #include <algorithm>
+#include <type_traits>
 #include "ycx_internal.h"
 
 namespace {
@@ -880,165 +881,241 @@ __global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
 
 // -------------------------------------------------------------------------
 // Stem + stride-2 conv, fused (yolov7's layers 0-1: 3x3 3->32, 3x3/s2 32->64).
-// A 256-thread block owns a 4 x 32 tile of the second conv's output and all
-// its (<= 64) channels:
+// Persistent 256-thread blocks (two per CU) walk a contiguous range of 4 x 32
+// tiles of the second conv's output, all its (<= 64) channels. Per block, once:
+// the second conv's weights (9 taps x this wave's 32 channels, 72 VGPRs) and
+// the stem's folded weights into registers. Per tile:
 //  (0) the fp32 image patch under the tile's 9 x 65 stem pixels (3 x 11 x 67
-//      floats at stem stride 1) is loaded into LDS with coalesced loads, all
-//      in flight at once, and the second conv's weights (all 9 taps of the
-//      wave's 32 channels) are requested into registers;
+//      floats at stem stride 1) sits in LDS, loaded into registers during the
+//      previous tile (row per wave-instruction, lane = column) and written
+//      after it; the patch rows / planes are padded (RS, CPS) so the stem's
+//      B gathers hit 2.5 instead of 4 LDS cycles per read;
 //  (1) the stem pixels are computed by MFMA (K = 27 <= 32, one instruction per
-//      16 pixels x 16 channels) from that patch and kept in LDS as bf16, 64 B
-//      per pixel, zero outside the stem map (the second conv's padding); even
-//      and odd stem columns live in separate planes so the B fragments of 16
+//      16 pixels x 16 channels), fully unrolled so a wave keeps several
+//      gathers / MFMAs / SiLUs in flight, and kept in LDS as bf16, 64 B per
+//      pixel, zero outside the stem map (the second conv's padding); even and
+//      odd stem columns live in separate planes so the B fragments of 16
 //      consecutive output pixels are 16 consecutive slots;
 //  (2) the second conv: one tap = one 32-deep MFMA step, B from the stem tile.
 // The 32-channel stem map (839 MB at bs = 32, 640^2) never touches HBM.
+// tests/probes/stem2_bench.py (bs 32, 640^2): 0.67 ms for the per-tile blocks
+// (stem phase alone 0.36: one dependent gather -> MFMA -> SiLU chain per wave).
 // -------------------------------------------------------------------------
 constexpr int kS2TH = 4, kS2TW = 32;                       // output tile
 constexpr int kS2R = 2 * kS2TH + 1, kS2C = 2 * kS2TW + 1;  // 9 x 65 stem pixels
 constexpr int kS2Even = (kS2C + 1) / 2, kS2Odd = kS2C / 2;
+constexpr int kS2Dump = kS2R * kS2C;  // one slot past the tile: writes of the pixels past it
 
 __device__ __forceinline__ int s2_slot(int r, int c) {
   return (c & 1) ? kS2R * kS2Even + r * kS2Odd + (c >> 1) : r * kS2Even + (c >> 1);
 }
+// 16-B chunk q of a stem pixel in plane column col lives at chunk q ^ s2_swz(col):
+// the stem phase's 16-B writes drop from 32 to 14 LDS cycles and the conv
+// phase's B reads from 8 to 4 (bank simulation over every access; the swizzle
+// depends on col & 7 only, so per conv lane it is one of two constants).
+__device__ __forceinline__ int s2_swz(int col) { return (col ^ ((col >> 1) & 2)) & 3; }
 
-template <int SS>  // stem stride
-__global__ void __launch_bounds__(256) stem2_fused(ConvArgs sa, ConvArgs ca) {
-  constexpr int NPIX = kS2R * kS2C, NGRP = (NPIX + 15) / 16;
+// Activation with the act code as a template argument (no per-element
+// branch); SiLU from the raw v_exp_f32 / v_rcp_f32 (bf16 outputs).
+template <int ACT>
+__device__ __forceinline__ float act_t(float v, float slope) {
+  if constexpr (ACT == YCX_ACT_SILU) return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.44269504f));
+  else if constexpr (ACT == YCX_ACT_LEAKY) return v > 0.0f ? v : v * slope;
+  else return v;
+}
+
+constexpr int s2_pad(int v, int m) { return v + ((m - v % 32) + 32) % 32; }  // smallest >= v, == m mod 32
+
+template <int SS, int ACT1, int ACT2>  // stem stride, stem / conv activation
+__global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) {
+  constexpr int NPIX = kS2R * kS2C, NGRP = (NPIX + 15) / 16, GPW = (NGRP + 3) / 4;
   constexpr int IR = (kS2R - 1) * SS + 3, IC = (kS2C - 1) * SS + 3;  // image patch rows / cols
-  constexpr int IMG = 3 * IR * IC;                                   // floats
+  constexpr int RS = s2_pad(IC, 7), CPS = s2_pad(IR * RS, 23);         // padded row / plane strides
+  constexpr int NROW = 3 * IR, RPW = (NROW + 3) / 4, NCH = (IC + 63) / 64;  // patch rows, per wave, 64-col chunks
   constexpr int FM = 2, FN = 4;  // per wave: 32 output channels x 64 pixels (2 rows x 32)
-  constexpr int STEM_BYTES = ((NPIX * 64) + 255) & ~255;
-  __shared__ __attribute__((aligned(1024))) char smem[STEM_BYTES + IMG * 4];
-  float* img = reinterpret_cast<float*>(smem + STEM_BYTES);
+  constexpr int STEM_BYTES = (((NPIX + 1) * 64) + 255) & ~255;  // + the dump slot
+  constexpr int IMGB = (3 * CPS * 4 + 255) & ~255;                  // one image patch buffer
+  __shared__ __attribute__((aligned(1024))) char smem[STEM_BYTES + 2 * IMGB];
   const int tid = threadIdx.x, lane = tid & 63, lx = lane & 15, kq = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wv & 1, wn = wv >> 1;  // 32-channel half, 2-row half
-  const int L = ycx_xcd_remap(blockIdx.x, ca.nwg);
-  const int tx_n = ca.Wo / kS2TW, tpi = (ca.Ho / kS2TH) * tx_n;
-  const int n = L / tpi, ti = L - n * tpi;
-  const int oy0 = (ti / tx_n) * kS2TH, ox0 = (ti % tx_n) * kS2TW;
-  const int sy0 = 2 * oy0 - 1, sx0 = 2 * ox0 - 1;          // stem pixel of tile slot (0, 0)
-  const int iy0 = sy0 * SS - sa.P, ix0 = sx0 * SS - sa.P;   // image pixel of patch (0, 0)
+  const int tx_n = ca.Wo / kS2TW, tpi = (ca.Ho / kS2TH) * tx_n, ntiles = ca.N * tpi;
+  const int blk = ycx_xcd_remap(blockIdx.x, gridDim.x);
+  const int tb = (int)((long long)blk * ntiles / gridDim.x), te = (int)((long long)(blk + 1) * ntiles / gridDim.x);
+  if (tb >= te) return;
 
-  // (0) weights of the second conv, all taps, this wave's 32 channels: A lane
-  //     (co = 32 wm + 16 i + lx, k = 32 t + 8 kq .. +7)
+  // second conv weights, all taps, this wave's 32 channels (A lane: co = 32 wm + 16 i + lx, k = 32 t + 8 kq ..)
   const __bf16* __restrict__ Wc = reinterpret_cast<const __bf16*>(ca.w);  // [Cout_pad][3][3][32]
-  constexpr int kAR = 3;  // taps of weights in flight (the first kAR requested before the stem phase)
-  auto load_a = [&](int t, bf16x8 (&a)[FM]) {
+  bf16x8 aw[9][FM];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int i = 0; i < FM; ++i)
-      a[i] = *reinterpret_cast<const bf16x8*>(Wc + (size_t)(32 * wm + 16 * i + lx) * ca.Ktot + 32 * t + 8 * kq);
-  };
-  bf16x8 aw[kAR][FM];
+      aw[t][i] = *reinterpret_cast<const bf16x8*>(Wc + (size_t)(32 * wm + 16 * i + lx) * ca.Ktot + 32 * t + 8 * kq);
+  f32x4 bvc[FM];
 #pragma unroll
-  for (int t = 0; t < kAR; ++t) load_a(t, aw[t]);
-  // ... and the image patch (fp32, zero outside the image)
-  {
-    const float* __restrict__ X = reinterpret_cast<const float*>(sa.x);
-    const float* Xn = X + (size_t)(n * sa.in_cs + sa.in_coff) * sa.H * sa.W;
-    constexpr int PER = (IMG + 255) / 256;
-    float v[PER];
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int e = u * 256 + tid;
-      const int c = e / (IR * IC), rem = e - c * (IR * IC), r = rem / IC, col = rem - r * IC;
-      const int iy = iy0 + r, ix = ix0 + col;
-      const bool ok = e < IMG && (unsigned)iy < (unsigned)sa.H && (unsigned)ix < (unsigned)sa.W;
-      v[u] = ok ? Xn[(size_t)c * sa.H * sa.W + iy * sa.W + ix] : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < PER; ++u)
-      if (u * 256 + tid < IMG) img[u * 256 + tid] = v[u];
+  for (int i = 0; i < FM; ++i) {
+    const int co = 32 * wm + 16 * i + 4 * kq;
+    bvc[i] = co < ca.Cout ? *reinterpret_cast<const f32x4*>(ca.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  __syncthreads();
-
-  // (1) stem tile
+  // stem weights / bias / gather offsets (k = 8 kq + j -> tap k / 3, channel k % 3; k >= 27 gathers
+  // what lane kq = 2 gathers, a broadcast, and weighs it 0)
+  constexpr int KT = 27, CIN = 3;
+  bf16x8 af[2];
+  int toff[8];
   {
-    constexpr int KT = 27, CIN = 3;
     const float* Ws = reinterpret_cast<const float*>(sa.w);  // [KT][Cout_pad]
-    bf16x8 af[2];
-    int toff[8];
-    bool kv[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = 8 * kq + j;
-      kv[j] = k < KT;
-      const int kk = kv[j] ? k : 0, tap = kk / CIN, dc = kk - tap * CIN;
-      const int dy = tap / 3, dx = tap - dy * 3;
-      toff[j] = (dc * IR + dy) * IC + dx;
+      const int k = 8 * kq + j, kv = k < KT, kk = kv ? k : 16 + j;
+      const int tap = kk / CIN, dc = kk - tap * CIN, dy = tap / 3, dx = tap - dy * 3;
+      toff[j] = dc * CPS + dy * RS + dx;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) af[t][j] = (__bf16)(kv[j] ? Ws[kk * sa.Cout_pad + stem_ch(t, lx)] : 0.0f);
+      for (int t = 0; t < 2; ++t) af[t][j] = (__bf16)(kv ? Ws[kk * sa.Cout_pad + stem_ch(t, lx)] : 0.0f);
     }
-    float bias[2][4];
+  }
+  f32x4 bias_s[2];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bias[t][r] = sa.bias[stem_ch(t, 4 * kq + r)];
-    // pixel p = 16 g + lx, g = wv, wv + 4, ...: (r, c) advance by 64 pixels per step
-    int pr = (16 * wv + lx) / kS2C, pcc = (16 * wv + lx) - pr * kS2C;
-    for (int g = wv; g < NGRP; g += 4) {
-      const int p = 16 * g + lx;
-      const int r = pr, c = pcc;
-      pcc += 64;
-      if (pcc >= kS2C) { pcc -= kS2C; ++pr; }  // 64 < kS2C: at most one wrap
-      const int sy = sy0 + r, sx = sx0 + c;
-      const bool inside = p < NPIX && (unsigned)sy < (unsigned)sa.Ho && (unsigned)sx < (unsigned)sa.Wo;
-      const float* ip = img + (p < NPIX ? (r * SS) * IC + c * SS : 0);  // tap (0, 0), channel 0
-      bf16x8 b;
+    for (int r = 0; r < 4; ++r) bias_s[t][r] = sa.bias[stem_ch(t, 4 * kq + r)];
+  // conv B reads: the chunk swizzle of plane column cc + d (d = kx / 2 on the even plane) is
+  // that of lx + d, 16 (j & 1) being a multiple of 8
+  const int swb0 = 16 * (kq ^ s2_swz(lx)), swb1 = 16 * (kq ^ s2_swz(lx + 1));
+
+  // image patch fetch: 4-byte LDS-DMA straight into one of two patch buffers
+  // (row q = (channel, row) per wave-instruction, lane = column); an element
+  // outside the image reads the descriptor's out-of-range zero
+  const int HWi = sa.H * sa.W;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)sa.x, (short)0, sa.N * sa.in_cs * HWi * 4, 0x00020000);
+  auto fetch = [&](int tile, int buf) {
+    const int n = tile / tpi, ti = tile - n * tpi;
+    const int iy0 = (2 * (ti / tx_n) * kS2TH - 1) * SS - sa.P, ix0 = (2 * (ti % tx_n) * kS2TW - 1) * SS - sa.P;
+    const int nb = (n * sa.in_cs + sa.in_coff) * HWi;
+    char* base = smem + STEM_BYTES + buf * IMGB;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) b[j] = (__bf16)(kv[j] ? ip[toff[j]] : 0.0f);
-      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], b, z, 0, 0, 0);
-      const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], b, z, 0, 0, 0);
+    for (int u = 0; u < RPW; ++u) {
+      const int q = wv + 4 * u, c = q / IR, r = q - c * IR, iy = iy0 + r;
+      if (q >= NROW) break;  // uniform
+      const bool rok = (unsigned)iy < (unsigned)sa.H;
+      const int rowb = nb + c * HWi + iy * sa.W;
+#pragma unroll
+      for (int h = 0; h < NCH; ++h) {
+        const int col = 64 * h + lane, ix = ix0 + col;
+        const bool ok = rok && (unsigned)ix < (unsigned)sa.W;
+        if (64 * h + 64 <= IC || col < IC)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(base + (c * CPS + r * RS + 64 * h) * 4), 4,
+                                                   ok ? (rowb + ix) * 4 : 0x7FFFFFF0, 0, 0, 0);
+      }
+    }
+  };
+  // stem phase addresses, the same for every tile: group g = wv + 4 u, pixel
+  // p = 16 g + lx -> image offset (floats) and stem-tile byte address (swizzled
+  // chunk kq); the pixels past the tile (p >= NPIX, last group) write a dump slot
+  int s_img[GPW], s_dst[GPW];
+#pragma unroll
+  for (int u = 0; u < GPW; ++u) {
+    const int p = 16 * (wv + 4 * u) + lx, ok = p < NPIX, pp = ok ? p : 0;
+    const int r = pp / kS2C, c = pp - r * kS2C;
+    s_img[u] = (r * SS) * RS + c * SS;
+    s_dst[u] = ok ? s2_slot(r, c) * 64 + 16 * (kq ^ s2_swz(c >> 1)) : kS2Dump * 64 + 16 * kq;
+  }
+  fetch(tb, 0);
+  __bf16* __restrict__ Y = reinterpret_cast<__bf16*>(ca.y) + ca.out_coff;
+  // the previous tile's epilogue issued exactly FM x FN stores per wave after
+  // this tile's fetch when every channel is stored (vmcnt counts in issue order)
+  const bool exact = ca.Cout == FM * 32;
+
+  for (int tile = tb; tile < te; ++tile) {
+    const int n = tile / tpi, ti = tile - n * tpi;
+    const int oy0 = (ti / tx_n) * kS2TH, ox0 = (ti % tx_n) * kS2TW;
+    const int sy0 = 2 * oy0 - 1, sx0 = 2 * ox0 - 1;  // stem pixel of tile slot (0, 0)
+    const float* img = reinterpret_cast<const float*>(smem + STEM_BYTES + ((tile - tb) & 1) * IMGB);
+    if (tile > tb && exact) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FM * FN) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // patch landed (every wave's share); stem tile free
+    if (tile + 1 < te) fetch(tile + 1, (tile + 1 - tb) & 1);
+
+    // (1) stem tile: group g = wv + 4 u covers pixels 16 g .. +15; the MFMA
+    //     accumulates onto the bias; branch-free so the unrolled groups overlap
+#pragma unroll
+    for (int u = 0; u < GPW; ++u) {
+      if (u == GPW - 1 && wv + 4 * u >= NGRP) break;  // uniform: the last group is one wave's
+      const float* ip = img + s_img[u];  // tap (0, 0), channel 0
+      bf16x8 bq;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bq[j] = (__bf16)ip[toff[j]];
+      const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bq, bias_s[0], 0, 0, 0);
+      const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bq, bias_s[1], 0, 0, 0);
       bf16x8 o;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {  // zero outside the stem map: the second conv's padding
-        o[q] = (__bf16)(inside ? ycx_act<true>(c0[q] + bias[0][q], sa.act, sa.slope) : 0.0f);
-        o[4 + q] = (__bf16)(inside ? ycx_act<true>(c1[q] + bias[1][q], sa.act, sa.slope) : 0.0f);
+      for (int q = 0; q < 4; ++q) {
+        o[q] = (__bf16)act_t<ACT1>(c0[q], sa.slope);
+        o[4 + q] = (__bf16)act_t<ACT1>(c1[q], sa.slope);
       }
-      if (p < NPIX) *reinterpret_cast<bf16x8*>(smem + s2_slot(r, c) * 64 + 16 * kq) = o;
+      *reinterpret_cast<bf16x8*>(smem + s_dst[u]) = o;
+      if (u & 1) __builtin_amdgcn_sched_barrier(0);  // two groups in flight: bounded registers
     }
-  }
-  __syncthreads();
+    // border tiles: stem pixels outside the stem map are the second conv's zero padding
+    const bool top = sy0 < 0, bottom = sy0 + kS2R > sa.Ho, left = sx0 < 0, right = sx0 + kS2C > sa.Wo;
+    if (top || bottom || left || right) {
+      __syncthreads();
+      const bf16x8 z8 = {};
+      for (int e = tid; e < (kS2R + kS2C) * 2 * 4; e += 256) {  // (row or column, pixel, 16-B chunk)
+        const int ch = e & 3, k = e >> 2;
+        int r = -1, c = -1;
+        if (k < kS2C) { r = top ? 0 : -1; c = k; }
+        else if (k < 2 * kS2C) { r = bottom ? sa.Ho - sy0 : -1; c = k - kS2C; }
+        else if (k < 2 * kS2C + kS2R) { c = left ? 0 : -1; r = k - 2 * kS2C; }
+        else { c = right ? sa.Wo - sx0 : -1; r = k - 2 * kS2C - kS2R; }
+        if (r >= 0 && c >= 0 && r < kS2R && c < kS2C)
+          *reinterpret_cast<bf16x8*>(smem + s2_slot(r, c) * 64 + 16 * (ch ^ s2_swz(c >> 1))) = z8;
+      }
+    }
+    __syncthreads();  // stem tile complete; patch free
 
-  // (2) second conv: wave (wm, wn) -> channels 32 wm.., output rows 2 wn, 2 wn + 1
-  //     (fragment j: row rr = 2 wn + (j >> 1), cols cc = 16 (j & 1) + lx). Its
-  //     stem pixel for tap (ky, kx) is (2 rr + ky, 2 cc + kx): even kx in the
-  //     even plane at slot (2 rr + ky) E + cc + kx/2, odd kx in the odd plane at
-  //     R E + (2 rr + ky) O + cc — per-lane bases plus per-tap constants.
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const char* be[FN];
-  const char* bo[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int rr = 2 * wn + (j >> 1), cc = 16 * (j & 1) + lx;
-    be[j] = smem + ((2 * rr) * kS2Even + cc) * 64 + 16 * kq;
-    bo[j] = smem + (kS2R * kS2Even + (2 * rr) * kS2Odd + cc) * 64 + 16 * kq;
-  }
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int ky = t / 3, kx = t - 3 * ky;
-    bf16x8 bfr[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-      bfr[j] = (kx & 1) ? *reinterpret_cast<const bf16x8*>(bo[j] + ky * kS2Odd * 64)
-                        : *reinterpret_cast<const bf16x8*>(be[j] + (ky * kS2Even + kx / 2) * 64);
+    // (2) second conv: wave (wm, wn) -> channels 32 wm.., output rows 2 wn, 2 wn + 1
+    //     (fragment j: row rr = 2 wn + (j >> 1), cols cc = 16 (j & 1) + lx). Its
+    //     stem pixel for tap (ky, kx) is (2 rr + ky, 2 cc + kx): even kx in the
+    //     even plane at slot (2 rr + ky) E + cc + kx/2, odd kx in the odd plane at
+    //     R E + (2 rr + ky) O + cc — per-lane bases plus per-tap constants.
+    f32x4 acc[FM][FN];  // accumulates onto the bias
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[t % kAR][i], bfr[j], acc[i][j], 0, 0, 0);
-    if (t + kAR < 9) load_a(t + kAR, aw[t % kAR]);
-  }
-  int pxf[FN];
+      for (int j = 0; j < FN; ++j) acc[i][j] = bvc[i];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) pxf[j] = n * ca.HoWo + (oy0 + 2 * wn + (j >> 1)) * ca.Wo + ox0 + 16 * (j & 1);
-  epilogue_frag<FM, FN>(ca, acc, 32 * wm, pxf, lane);
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t - 3 * ky;
+      bf16x8 bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int rr = 2 * wn + (j >> 1), cc = 16 * (j & 1) + lx;
+        const int slot = (kx & 1) ? kS2R * kS2Even + (2 * rr + ky) * kS2Odd + cc : (2 * rr + ky) * kS2Even + cc + kx / 2;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(smem + slot * 64 + (kx == 2 ? swb1 : swb0));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[t][i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    // epilogue: bias + act, 8-byte stores (4 channels of one pixel per lane)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int co = 32 * wm + 16 * i + 4 * kq;
+      if (co >= ca.Cout) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int p = n * ca.HoWo + (oy0 + 2 * wn + (j >> 1)) * ca.Wo + ox0 + 16 * (j & 1) + lx;
+        bf16x4 ov;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ov[q] = (__bf16)act_t<ACT2>(acc[i][j][q], ca.slope);
+        *reinterpret_cast<bf16x4*>(Y + (size_t)p * ca.out_cs + co) = ov;
+      }
+    }
+  }
 }
 
 // -------------------------------------------------------------------------
@@ -1503,11 +1580,21 @@ extern "C" ycx_status ycx_stem_conv2(const ycx_conv_desc* sd, const ycx_conv_des
   YCX_CHECK_SUPPORTED((long long)cd->n * cd->ho * cd->wo < (1LL << 31));
   ConvArgs sa = make_args(sd, x, w_stem, b_stem, nullptr, nullptr);
   ConvArgs ca = make_args(cd, nullptr, w_conv, b_conv, y, nullptr);
-  ca.nwg = cd->n * (cd->ho / kS2TH) * (cd->wo / kS2TW);
+  const long long ntiles = (long long)cd->n * (cd->ho / kS2TH) * (cd->wo / kS2TW);
+  ca.nwg = (int)std::min<long long>(ntiles, 2 * 256);  // persistent: two blocks per CU
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (sd->stride == 1)
-    hipLaunchKernelGGL((stem2_fused<1>), dim3(ca.nwg), dim3(256), 0, st, sa, ca);
-  else
-    hipLaunchKernelGGL((stem2_fused<2>), dim3(ca.nwg), dim3(256), 0, st, sa, ca);
-  return ycx_launch_status();
+  const dim3 g(ca.nwg), b(256);
+#define YCX_STEM2(SS_, A1_, A2_)                                                           \
+  if (sd->stride == SS_ && sd->act == A1_ && cd->act == A2_) {                            \
+    hipLaunchKernelGGL((stem2_fused<SS_, A1_, A2_>), g, b, 0, st, sa, ca);                \
+    return ycx_launch_status();                                                           \
+  }
+  YCX_STEM2(1, YCX_ACT_SILU, YCX_ACT_SILU)
+  YCX_STEM2(1, YCX_ACT_LEAKY, YCX_ACT_LEAKY)
+  YCX_STEM2(1, YCX_ACT_NONE, YCX_ACT_NONE)
+  YCX_STEM2(2, YCX_ACT_SILU, YCX_ACT_SILU)
+  YCX_STEM2(2, YCX_ACT_LEAKY, YCX_ACT_LEAKY)
+  YCX_STEM2(2, YCX_ACT_NONE, YCX_ACT_NONE)
+#undef YCX_STEM2
+  return YCX_ERR_UNSUPPORTED;
 }

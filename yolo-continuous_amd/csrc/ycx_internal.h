@@ -25,12 +25,14 @@ static inline ycx_status ycx_launch_status() {
 static inline unsigned ycx_cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
 
 // Activation applied in the conv epilogues (Conv.act, nets/common.py:103).
-// FAST (bf16 outputs): v_exp + v_rcp (~1 ulp fp32, far below bf16 rounding);
-// otherwise the IEEE division of torch's silu for the f32 parity mode.
+// FAST (bf16 outputs): the raw v_exp_f32 (2^x, no range fix-up: overflow to
+// inf gives rcp 0, i.e. silu -> 0) and v_rcp_f32, ~1 ulp fp32, far below bf16
+// rounding; otherwise the IEEE division of torch's silu for the f32 parity mode.
 template <bool FAST>
 __device__ __forceinline__ float ycx_act(float v, int act, float slope) {
-  if (act == YCX_ACT_SILU)
-    return FAST ? v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)) : v / (1.0f + expf(-v));  // x*sigmoid(x)
+  if (act == YCX_ACT_SILU)  // x*sigmoid(x)
+    return FAST ? v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.44269504f))
+                : v / (1.0f + expf(-v));
   if (act == YCX_ACT_LEAKY) return v > 0.0f ? v : v * slope;
   return v;
 }

@@ -442,6 +442,8 @@ class Engine:
             if not (q['k'] == 3 and q['s'] == 2 and q['p'] == 1 and int(q['w'].shape[0]) <= 64 and
                     int(q['w'].shape[0]) % 8 == 0 and q['ho'] % 4 == 0 and q['wo'] % 32 == 0):
                 continue
+            if p['act'] != q['act']:  # the fused kernel is instantiated per (act, act) with both equal
+                continue
             pairs[id(nd)] = c
         return pairs
 
