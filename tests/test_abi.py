@@ -49,7 +49,10 @@ def test_tile_picker():
     d.n, d.ho, d.wo, d.cin, d.cout_pad, d.dtype = 32, 160, 160, 64, 64, _lib.DT_BF16
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 15   # 512-thread 2-stage LDS-DMA co64 x px256
     d.h, d.w, d.kh, d.kw, d.stride, d.pad = 160, 160, 3, 3, 1, 1
-    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 19   # 3x3 s1: LDS halo tile
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 23   # 3x3 s1 64->64: weight-stationary halo
+    d.res_c_stride = 64
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 19   # ... with a residual: LDS halo tile
+    d.res_c_stride = 0
     d.cout_pad = 128
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 20
     d.cout_pad, d.kh, d.kw, d.pad = 64, 1, 1, 0

@@ -112,6 +112,15 @@ def test_conv1x1_wres_multi_tile(device, n, hw, cin, cout):
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize('n,hw,cout,act', [(2, (16, 16), 64, L.ACT_SILU), (2, (32, 48), 64, L.ACT_LEAKY),
+                                           (3, (64, 80), 48, L.ACT_SILU), (1, (16, 32), 64, L.ACT_NONE)])
+def test_conv3x3_ws64(device, n, hw, cout, act):
+    """Weight-stationary 3x3 64->64 kernel (tile 23): image borders as halo zeros,
+    several tiles per persistent block (double-buffered halo), sliced channels."""
+    got, ref = _run_conv(device, n, hw[0], hw[1], 64, cout, 3, 1, act, 23, L.DT_BF16, in_extra=8, out_extra=16)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+
+
 def test_conv_halo3x3_residual_up2(device):
     got, ref = _run_conv(device, 1, 32, 16, 64, 64, 3, 1, L.ACT_LEAKY, 19, L.DT_BF16, residual=True)
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=2e-2)

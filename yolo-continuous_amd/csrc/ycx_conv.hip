@@ -521,6 +521,125 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
 // 16 distinct bank slots per LDS cycle (brute-forced over every halo offset).
 // Requires H == Ho, W == Wo, Ho % 16 == Wo % 16 == 0, Cin % 64 == 0.
 // -------------------------------------------------------------------------
+// -------------------------------------------------------------------------
+// 3x3/s1 conv, 64 -> 64 channels, weight-stationary (yolov7's 320^2 / 160^2
+// ELAN 3x3s): the per-tile halo kernel above pulls all nine taps of weights
+// (72 KB) into LDS for every 16x16 tile, more bytes than the tile's halo
+// (41.5 KB); at 320^2 that is 0.94 GB of L2 -> LDS traffic per layer. Here
+// one 512-thread block per CU loads the weights into LDS once ([tap][co] rows
+// of 128 B, chunk-swizzled as the im2col tiles' A image) and walks a
+// contiguous range of tiles; the halo of tile i + 1 is DMA'd into the second
+// of two halo buffers while tile i computes (no barrier inside a tile). Wave
+// (wm, wn): channels 32 wm .. +31, tile rows 4 wn .. +3. The epilogue's
+// FM x FN stores per wave are counted into the next tile's wait.
+// Requires Cin == Cout_pad == 64, H == Ho, W == Wo, both % 16 == 0, NHWC bf16
+// output without residual.
+// -------------------------------------------------------------------------
+template <int ACT>
+__global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
+  constexpr int NW = 8, TH = 16, TW = 16, HW = TW + 2, HP = (TH + 2) * HW;  // 324 halo pixels
+  constexpr int HPIECES = (HP + 7) / 8, HPW = (HPIECES + NW - 1) / NW;     // 1-KB DMA pieces (8 pixels)
+  constexpr int HBUF = HPIECES * 1024, WBYTES = 9 * 64 * 128;
+  constexpr int FM = 2, FN = 4;
+  __shared__ __attribute__((aligned(1024))) char smem[WBYTES + 2 * HBUF];
+  char* const wl = smem;
+  const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
+  const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int tx_n = a.Wo / TW, tpi = (a.Ho / TH) * tx_n, ntiles = a.N * tpi;
+  const int blk = ycx_xcd_remap(blockIdx.x, gridDim.x);
+  const int tb = (int)((long long)blk * ntiles / gridDim.x), te = (int)((long long)(blk + 1) * ntiles / gridDim.x);
+  if (tb >= te) return;
+  const int w_bytes = a.Cout_pad * a.Ktot * 2, x_bytes = a.N * a.H * a.W * a.in_cs * 2;
+
+  // weights: LDS row R = 64 tap + co (128 B), logical chunk q at q ^ swz(co); 72 pieces, 9 per wave
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int R = 8 * (wid + NW * i) + lrow, t = R >> 6, co = R & 63;
+    buf_lds16(Wt, w_bytes, (co * a.Ktot + t * 64 + ((pch ^ swz<64>(co)) << 3)) * 2, 0, wl + (wid + NW * i) * 1024);
+  }
+  // halo of a tile into buffer b: halo pixel h keeps its chunk q at q ^ (h & 7)
+  auto issue_h = [&](int tile, int b) {
+    const int n = tile / tpi, ti = tile - n * tpi;
+    const int oy0 = (ti / tx_n) * TH, ox0 = (ti % tx_n) * TW;
+#pragma unroll
+    for (int i = 0; i < HPW; ++i) {
+      const int piece = wid + NW * i;
+      if (piece >= HPIECES) break;  // uniform
+      const int h = 8 * piece + lrow, hy = h / HW, hx = h - hy * HW;
+      const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
+      const bool ok = h < HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      buf_lds16(X, x_bytes, ok ? (((n * a.H + iy) * a.W + ix) * a.in_cs + a.in_coff + ((pch ^ (h & 7)) << 3)) * 2
+                               : 0x7FFFFFF0, 0, smem + WBYTES + b * HBUF + piece * 1024);
+    }
+  };
+  issue_h(tb, 0);
+  f32x4 bv[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int co = 32 * wm + 16 * i + 4 * (lane >> 4);
+    bv[i] = co < a.Cout ? *reinterpret_cast<const f32x4*>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bool exact = a.Cout == 64;  // then every tile stores FM x FN times per wave
+  __bf16* __restrict__ Y = reinterpret_cast<__bf16*>(a.y) + a.out_coff;
+
+  for (int tile = tb; tile < te; ++tile) {
+    const int b = (tile - tb) & 1;
+    if (tile > tb && exact) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FM * FN) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // this tile's halo (and the weights) landed; the other buffer is free
+    if (tile + 1 < te) issue_h(tile + 1, b ^ 1);
+    const char* halo = smem + WBYTES + b * HBUF;
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = bv[i];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t - 3 * ky;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int lc = kk * 4 + (lane >> 4);
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int co = 32 * wm + 16 * i + (lane & 15);
+          af[i] = *reinterpret_cast<const bf16x8*>(wl + (t * 64 + co) * 128 + ((lc ^ swz<64>(co)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int h = (wn * FN + j + ky) * HW + (lane & 15) + kx;
+          bfr[j] = *reinterpret_cast<const bf16x8*>(halo + h * 128 + ((lc ^ (h & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    // epilogue: act, 8-byte stores from registers (no global loads: they would drain vmcnt)
+    const int n = tile / tpi, ti = tile - n * tpi;
+    const int oy0 = (ti / tx_n) * TH, ox0 = (ti % tx_n) * TW;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int co = 32 * wm + 16 * i + 4 * (lane >> 4);
+      if (co >= a.Cout) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int p = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0 + (lane & 15);
+        bf16x4 ov;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ov[q] = (__bf16)act_t<ACT>(acc[i][j][q], a.slope);
+        *reinterpret_cast<bf16x4*>(Y + (size_t)p * a.out_cs + co) = ov;
+      }
+    }
+  }
+}
+
 template <int BM, int WM, int WN, int NSTA>
 __global__ void __launch_bounds__(WM * WN * 64) conv3x3_halo(ConvArgs a) {
   constexpr int NW = WM * WN;
@@ -915,15 +1034,6 @@ __device__ __forceinline__ int s2_slot(int r, int c) {
 // depends on col & 7 only, so per conv lane it is one of two constants).
 __device__ __forceinline__ int s2_swz(int col) { return (col ^ ((col >> 1) & 2)) & 3; }
 
-// Activation with the act code as a template argument (no per-element
-// branch); SiLU from the raw v_exp_f32 / v_rcp_f32 (bf16 outputs).
-template <int ACT>
-__device__ __forceinline__ float act_t(float v, float slope) {
-  if constexpr (ACT == YCX_ACT_SILU) return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.44269504f));
-  else if constexpr (ACT == YCX_ACT_LEAKY) return v > 0.0f ? v : v * slope;
-  else return v;
-}
-
 constexpr int s2_pad(int v, int m) { return v + ((m - v % 32) + 32) % 32; }  // smallest >= v, == m mod 32
 
 template <int SS, int ACT1, int ACT2>  // stem stride, stem / conv activation
@@ -1314,6 +1424,7 @@ const TileInfo kTiles[] = {
     {128, 256, 64, "halo3x3_co128_t16x16_s2"},
     {128, 256, 64, "halo3x3_co128_t16x16_s3"},
     {32, 64, 64, "wres1x1"},
+    {64, 256, 64, "halo3x3_ws_co64"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -1324,6 +1435,25 @@ ycx_status launch_bf16(ConvArgs a, hipStream_t st) {
   int n_pt = (a.M + BN - 1) / BN;
   a.nwg = a.n_ct * n_pt;
   hipLaunchKernelGGL((conv_bf16_kernel<BM, BN, BK, WM, WN>), dim3(a.nwg), dim3(256), 0, st, a);
+  return ycx_launch_status();
+}
+
+bool ws64_ok(const ConvArgs& a) {
+  return a.KH == 3 && a.KW == 3 && a.S == 1 && a.P == 1 && a.H == a.Ho && a.W == a.Wo && a.Ho % 16 == 0 &&
+         a.Wo % 16 == 0 && a.Cin == 64 && a.Cout_pad == 64 && a.out_layout == YCX_OUT_NHWC && !a.res &&
+         (long long)a.N * a.H * a.W * a.in_cs * 2 < (1LL << 31) - 64;
+}
+
+// tile 23: one persistent block per CU
+ycx_status launch_ws64(ConvArgs a, hipStream_t st) {
+  if (!ws64_ok(a)) return YCX_ERR_UNSUPPORTED;
+  const long long ntiles = (long long)a.N * (a.Ho / 16) * (a.Wo / 16);
+  const dim3 g((unsigned)std::min<long long>(ntiles, 256)), b(512);
+  switch (a.act) {
+    case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_SILU>), g, b, 0, st, a); break;
+    case YCX_ACT_LEAKY: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_LEAKY>), g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_NONE>), g, b, 0, st, a); break;
+  }
   return ycx_launch_status();
 }
 
@@ -1393,7 +1523,7 @@ extern "C" const char* ycx_conv_tile_name(int32_t tile) {
 
 // Tile heuristic: pick the largest tile that still gives >= ~2 waves of blocks
 // on 256 CUs, with BK = 32 only where cin is not a multiple of 64.
-static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {
+static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wres: no residual (tiles 22, 23)
   if (d->dtype == YCX_DT_F32) return 8;
   const long long M = (long long)d->n * d->ho * d->wo;
   const bool k64 = (d->cin % 64) == 0;
@@ -1424,6 +1554,11 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {
   // +14-18 % over the im2col tiles at 80^2 with >= 128 output channels, +18 % at 320^2 x 64)
   if (d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->h == d->ho && d->w == d->wo &&
       d->ho % 16 == 0 && d->wo % 16 == 0 && d->out_layout != YCX_OUT_NCHW_F32) {
+    // 64 -> 64: weights resident in LDS across a persistent block's tiles (tile 23:
+    // 320^2 0.43 -> 0.28 ms, 160^2 0.10 -> 0.06 ms at bs 32); needs >= 2 tiles per block
+    if (allow_wres && d->cin == 64 && d->cout_pad == 64 && d->out_layout == YCX_OUT_NHWC &&
+        (long long)d->n * (d->ho / 16) * (d->wo / 16) >= 512)
+      return 23;
     if (d->cout_pad % 128 == 0) return 20;
     if (d->cout_pad == 64 && d->ho >= 160) return 19;
   }
@@ -1500,6 +1635,7 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
     case 20: return launch_halo<128, 2, 4, 2>(a, st);
     case 21: return launch_halo<128, 2, 4, 3>(a, st);
     case 22: return launch_wres(a, st);
+    case 23: return launch_ws64(a, st);
     default: return YCX_ERR_UNSUPPORTED;
   }
 }

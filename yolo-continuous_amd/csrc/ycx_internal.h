@@ -37,6 +37,14 @@ __device__ __forceinline__ float ycx_act(float v, int act, float slope) {
   return v;
 }
 
+// The same with the act code as a template argument (no per-element branch).
+template <int ACT>
+__device__ __forceinline__ float act_t(float v, float slope) {
+  if constexpr (ACT == YCX_ACT_SILU) return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.44269504f));
+  else if constexpr (ACT == YCX_ACT_LEAKY) return v > 0.0f ? v : v * slope;
+  else return v;
+}
+
 // XCD-aware bijective remap of a 1-D block id (guide §5 "XCD swizzle must be
 // bijective"): consecutive logical ids land on the same XCD (blocks b, b+8, ...
 // share one), so blocks that share an activation tile share an L2.
