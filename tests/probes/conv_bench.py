@@ -34,6 +34,13 @@ SHAPES = [  # n, h, w, cin, cout, k, s
     (32, 80, 80, 512, 256, 1, 1),
     (32, 80, 80, 512, 128, 1, 1),
     (32, 40, 40, 512, 512, 1, 1),
+    (32, 20, 20, 256, 256, 3, 1),
+    (32, 20, 20, 512, 256, 3, 1),
+    (32, 40, 40, 256, 256, 3, 2),
+    (32, 20, 20, 512, 256, 1, 1),
+    (32, 40, 40, 256, 128, 1, 1),
+    (32, 20, 20, 512, 1024, 3, 1),
+    (32, 40, 40, 256, 512, 3, 1),
 ]
 
 

@@ -1564,7 +1564,9 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
   }
   if (d->cout_pad % 128 == 0) {
     if ((d->cout_pad / 128) * ((M + 127) / 128) >= 256) return 16;
-    return 4;  // co128 x px64, 256 threads: more blocks for small-M (deep) layers
+    // small-M (deep) layers: co64 x px128 LDS-DMA blocks, two per CU (tests/probes/conv_bench.py,
+    // 20^2 x bs 32: 3x3 256->256 0.037 -> 0.027 ms, 512->256 0.068 -> 0.046 ms against co128 x px64)
+    return 18;
   }
   if ((M + 255) / 256 >= 2048) return 15;
   if ((d->cout_pad / 64) * ((M + 127) / 128) >= 256) return 18;
