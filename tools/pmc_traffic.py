@@ -20,19 +20,21 @@ import csv
 import glob
 import json
 import os
+import re
 
-OURS = ("conv_bf16_glds", "conv3x3_halo", "conv_bf16_kernel", "conv_f32_kernel", "stem2_fused", "stem_mfma",
-        "stem_kernel", "maxpool_kernel", "copy_kernel", "decode_filter_kernel", "decode_kernel", "idetect_kernel",
-        "filter_decoded_kernel", "nms_prep", "nms_big", "nms_finish", "letterbox_kernel", "correct_boxes_kernel")
 KIB = 1024
 
 
 def _short(name):
-    # names arrive demangled ("(anonymous namespace)::nms_mask(...)") or, when the
-    # demangler gives up on __bf16 template arguments, mangled ("_ZN12_GLOBAL__N_111copy_kernelIDF16b...")
-    for k in OURS:
-        if k in name:
-            return k
+    """Base name of one of our kernels (all live in anonymous namespaces), else None.
+    Names arrive demangled ("void (anonymous namespace)::conv1x1_wres<8, ...>(...)") or, when
+    the demangler gives up on __bf16 template arguments, mangled ("_ZN12_GLOBAL__N_111copy_kernelI...")."""
+    if "(anonymous namespace)::" in name:
+        return re.split(r"[<(]", name.split("(anonymous namespace)::", 1)[1], 1)[0]
+    m = re.match(r"_ZN12_GLOBAL__N_1(\d+)", name)
+    if m:
+        n = int(m.group(1))
+        return name[m.end():m.end() + n]
     return None
 
 
