@@ -485,26 +485,32 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
     if (t + NST - 1 < nt) issue(t + NST - 1, (t + NST - 1) % NST);
     const __bf16* A = reinterpret_cast<const __bf16*>(smem + (t % NST) * STAGE);
     const __bf16* B = reinterpret_cast<const __bf16*>(smem + (t % NST) * STAGE + A_BYTES);
+    // all of the stage's fragments are requested before the first MFMA (left to
+    // itself the compiler re-reads fragments between MFMAs to save registers,
+    // exposing an LDS latency every two MFMAs)
+    bf16x8 af[BK / 32][FM], bfr[BK / 32][FN];
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       const int c = kk * 4 + (lane >> 4);
-      bf16x8 af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int row = wm * TM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(A + row * BK + ((c ^ swz<BK>(row)) << 3));
+        af[kk][i] = *reinterpret_cast<const bf16x8*>(A + row * BK + ((c ^ swz<BK>(row)) << 3));
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int row = wn * TN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(B + row * BK + ((c ^ swz<BK>(row)) << 3));
+        bfr[kk][j] = *reinterpret_cast<const bf16x8*>(B + row * BK + ((c ^ swz<BK>(row)) << 3));
       }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
   epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
@@ -1425,6 +1431,9 @@ const TileInfo kTiles[] = {
     {128, 256, 64, "halo3x3_co128_t16x16_s3"},
     {32, 64, 64, "wres1x1"},
     {64, 256, 64, "halo3x3_ws_co64"},
+    {256, 256, 64, "glds_co256_px256_k64_s2"},
+    {256, 128, 64, "glds_co256_px128_k64_s2"},
+    {128, 256, 64, "glds_co128_px256_k64_s2"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -1638,6 +1647,9 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
     case 21: return launch_halo<128, 2, 4, 3>(a, st);
     case 22: return launch_wres(a, st);
     case 23: return launch_ws64(a, st);
+    case 24: return launch_glds<256, 256, 2, 4, false, 2>(a, st);
+    case 25: return launch_glds<256, 128, 2, 4, false, 2>(a, st);
+    case 26: return launch_glds<128, 256, 2, 4, false, 2>(a, st);
     default: return YCX_ERR_UNSUPPORTED;
   }
 }
