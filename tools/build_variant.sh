@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build an experiment variant of libycx_hip.so (development tool):
+#   bash tools/build_variant.sh NAME -DFLAG ...  ->  yolo-continuous_amd/csrc/build/libycx_NAME.so
+set -e
+cd "$(dirname "$0")/../yolo-continuous_amd/csrc"
+make -s
+NAME=$1; shift
+mkdir -p build/var
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -Wno-unused-function "$@" \
+  -c ycx_conv.hip -o build/var/ycx_conv_$NAME.o 2>/dev/null
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC build/var/ycx_conv_$NAME.o build/ycx_misc.o build/ycx_post.o \
+  build/ycx_nms.o build/ycx_image.o -o build/libycx_$NAME.so
+echo build/libycx_$NAME.so
