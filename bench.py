@@ -47,6 +47,10 @@ def parse(argv=None):
     ap.add_argument("--nc", type=int, default=80)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--mode", default="concurrent", choices=["concurrent", "pipelined", "serial"],
+                    help="concurrent: 3 batches in flight on 3 streams (default); pipelined: forward and "
+                         "decode+NMS on two streams; serial: one stream")
+    ap.add_argument("--depth", type=int, default=3, help="batches in flight in concurrent mode")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each batch's forward and post back to back on one stream")
     ap.add_argument("--conf", type=float, default=0.3)
@@ -135,9 +139,10 @@ def cpu_baseline(args, sd, model_cfg, budget_s):
 
 def setup(args, dev, rank=0, use_graph=None, pipeline=False):
     """The bench workload on ``dev``: yolov7 with seeded synthetic weights, a
-    Detector (or a 2-slot PipelinedDetector) for (batch, 3, size, size) and
-    this rank's synthetic images already resident in HBM."""
-    from ycx.detect import Detector, PipelinedDetector
+    Detector (pipeline False), a 2-slot PipelinedDetector ('pipelined') or a
+    ConcurrentDetector ('concurrent' / True) for (batch, 3, size, size) and this
+    rank's synthetic images already resident in HBM."""
+    from ycx.detect import ConcurrentDetector, Detector, PipelinedDetector
     from ycx.nets.yolo import Model
     from ycx.utils.helper_io import cvt_cfg
     from ycx.utils.synth import synthetic_images, synthetic_state_dict
@@ -152,7 +157,10 @@ def setup(args, dev, rank=0, use_graph=None, pipeline=False):
               use_graph=(not args.no_graph) if use_graph is None else use_graph)
     images = synthetic_images(*shape, seed=1000 + rank).to(dev)
     if pipeline:
-        det = PipelinedDetector(model, shape, dev, ANCHORS, MASK, depth=2, **kw)
+        if pipeline == 'pipelined':
+            det = PipelinedDetector(model, shape, dev, ANCHORS, MASK, depth=2, **kw)
+        else:
+            det = ConcurrentDetector(model, shape, dev, ANCHORS, MASK, depth=getattr(args, 'depth', 3), **kw)
         for d in det.slots:
             d.x.copy_(images)
     else:
@@ -187,14 +195,25 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    pipeline = not args.no_pipeline
+    mode = "serial" if args.no_pipeline else args.mode
+    pipeline = False if mode == "serial" else mode
     model, det, sd, cfg, shape = setup(args, dev, rank, pipeline=pipeline)
     from ycx.dist import gather_detections
+    s_coll = torch.cuda.Stream(dev) if (world > 1 and mode == "concurrent") else None
     lat_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
 
     def step(i=None):
         timing = lat_ev[i] if i is not None else None
+        if mode == "concurrent":
+            dets, keep, kc, done = det.submit(timing=(timing[0], None) if (timing and world > 1) else timing)
+            if world > 1:  # the single collective, in batch order on one stream (same order on every rank)
+                with torch.cuda.stream(s_coll):
+                    s_coll.wait_event(done)
+                    dets, kc, keep = gather_detections(dets, kc, keep)
+                    if timing is not None:
+                        timing[1].record(s_coll)
+            return kc
         if pipeline:
             dets, keep, kc, _ = det.submit(timing=timing)
             if world > 1:  # the single collective, on the post stream after this batch's NMS
@@ -213,6 +232,8 @@ def main():
     def drain():
         if pipeline:
             det.synchronize()
+        if s_coll is not None:
+            torch.cuda.current_stream().wait_stream(s_coll)
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -253,7 +274,8 @@ def main():
                                    f"per step: forward + decode + NMS (+ all-gather)",
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch, "image_size": args.size,
                        "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
-                       "pipelined_streams": pipeline,
+                       "mode": mode, "batches_in_flight": (args.depth if mode == "concurrent" else
+                                                           2 if mode == "pipelined" else 1),
                        "conf_thres": args.conf, "iou_thres": args.iou, "max_det": args.max_det},
             "mfma_fraction_whole_step": round(model.engine_for(shape, dev).flops_per_image * value /
                                               (world * peak * 1e12), 4),

@@ -43,5 +43,41 @@ def main():
         print(f"pipelined post-priority {prio}: {timed(pd.submit, n=30):.3f} ms/step", flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and sys.argv[1:2] != ["concurrent"]:
     main()
+
+
+class Concurrent:
+    """Each slot has its own stream; a batch's forward + post run on its slot's stream,
+    so consecutive batches' forwards overlap (fills each other's kernel tails)."""
+
+    def __init__(self, model, shape, dev, depth, prio=(0,), **kw):
+        from ycx.detect import Detector
+        self.slots = [Detector(model, shape, dev, bench.ANCHORS, bench.MASK, slot=k, **kw) for k in range(depth)]
+        self.streams = [torch.cuda.Stream(dev, priority=prio[k % len(prio)]) for k in range(depth)]
+        self.i = 0
+
+    def submit(self):
+        k = self.i % len(self.slots)
+        self.i += 1
+        with torch.cuda.stream(self.streams[k]):
+            self.slots[k].forward()
+            return self.slots[k].post()
+
+
+def concurrent_main():
+    args = bench.parse([])
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    model, det, _, _, _ = bench.setup(args, dev)
+    shape = (args.batch, 3, args.size, args.size)
+    kw = dict(conf_thres=args.conf, nms_thres=args.iou, max_det=args.max_det)
+    for depth, prio in ((2, (0,)), (2, (0, -1)), (3, (0,)), (3, (0, -1)), (4, (0,)), (4, (0, -1))):
+        c = Concurrent(model, shape, dev, depth, prio, **kw)
+        print(f"concurrent depth {depth} prio {prio}: {timed(c.submit, n=30):.3f} ms/step", flush=True)
+        del c
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__" and sys.argv[1:2] == ["concurrent"]:
+    concurrent_main()

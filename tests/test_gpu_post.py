@@ -11,7 +11,7 @@ import torch
 
 from helpers import ANCHORS, MASK, g3_heads, make_model, rel_err
 from oracle import ref_forward, ref_post
-from ycx.detect import Detector, PipelinedDetector, decode_box, nms_device, non_max_suppression
+from ycx.detect import ConcurrentDetector, Detector, PipelinedDetector, decode_box, nms_device, non_max_suppression
 from ycx.utils.helper_io import cvt_cfg
 from ycx.utils.synth import synthetic_images
 
@@ -161,6 +161,27 @@ def test_pipelined_detector_matches_serial(device):
         torch.cuda.current_stream().wait_event(done)
         got.append([dets.clone(), keep.clone(), kc.clone()])
     pd.synchronize()
+    torch.cuda.synchronize()
+    for (d1, k1, c1), (d2, k2, c2) in zip(want, got):
+        assert torch.equal(c1, c2) and torch.equal(k1, k2) and torch.equal(d1, d2)
+
+
+def test_concurrent_detector_matches_serial(device):
+    """Three slots on three streams, seven batches back to back (every slot
+    reused): each batch's detections equal the single-stream Detector's."""
+    m, _ = make_model('yolov7-tiny', 1, 0, 'bf16')
+    m.to(device)
+    shape = (2, 3, 256, 256)
+    ref = Detector(m, shape, device, ANCHORS, MASK, use_graph=True)
+    cd = ConcurrentDetector(m, shape, device, ANCHORS, MASK, depth=3, use_graph=True)
+    xs = [synthetic_images(*shape, seed=40 + i).to(device) for i in range(7)]
+    want = [[t.clone() for t in ref(x)] for x in xs]
+    got = []
+    for x in xs:
+        dets, keep, kc, done = cd.submit(x)
+        torch.cuda.current_stream().wait_event(done)
+        got.append([dets.clone(), keep.clone(), kc.clone()])
+    cd.synchronize()
     torch.cuda.synchronize()
     for (d1, k1, c1), (d2, k2, c2) in zip(want, got):
         assert torch.equal(c1, c2) and torch.equal(k1, k2) and torch.equal(d1, d2)

@@ -318,6 +318,53 @@ class PipelinedDetector:
         cur.wait_stream(self.s_post)
 
 
+class ConcurrentDetector:
+    """``depth`` batches in flight, each on its own slot and HIP stream: batch i
+    runs forward + decode + NMS on stream i % depth, so consecutive batches'
+    kernels interleave on the GPU and fill each other's tails (the last, partly
+    empty wave of blocks of every conv, the small 20^2/40^2 layers, the
+    one-block-per-class NMS). Same interface as PipelinedDetector; a slot's
+    outputs stay valid until the slot is submitted again (``depth`` batches
+    later). Throughput-oriented: the per-batch latency grows with depth.
+
+    depth 3: HIP spreads streams over GPU_MAX_HW_QUEUES (4) hardware queues and
+    two same-priority streams may share one; with three, at least two batches
+    always run concurrently (tests/probes/step_split.py concurrent)."""
+
+    def __init__(self, model, shape, device, anchors, anchors_mask, depth=3, **kw):
+        self.device = torch.device(device)
+        self.slots = [Detector(model, shape, device, anchors, anchors_mask, slot=k, **kw) for k in range(depth)]
+        self.streams = [torch.cuda.Stream(self.device, priority=0) for _ in self.slots]
+        self.done = [torch.cuda.Event() for _ in self.slots]
+        self.i = 0
+
+    @property
+    def s_post(self):  # the stream of the most recent batch (where its collective goes)
+        return self.streams[(self.i - 1) % len(self.slots)]
+
+    def submit(self, images=None, timing=None):
+        k = self.i % len(self.slots)
+        self.i += 1
+        det, s = self.slots[k], self.streams[k]
+        s.wait_stream(torch.cuda.current_stream(self.device))  # caller's inputs are ready
+        with torch.cuda.stream(s):
+            if timing is not None:
+                timing[0].record(s)
+            if images is not None:
+                det.x.copy_(images)
+            det.forward()
+            dets, keep, kc = det.post()
+            self.done[k].record(s)
+            if timing is not None and timing[1] is not None:
+                timing[1].record(s)
+        return dets, keep, kc, self.done[k]
+
+    def synchronize(self):
+        cur = torch.cuda.current_stream(self.device)
+        for s in self.streams:
+            cur.wait_stream(s)
+
+
 def prepare_model(plan, weights=None, device=None, precision='bf16'):
     """detect.py:168-180: build the Model from the plan and load its weights.
     ``weights`` overrides plan.save_path (a state_dict or a path, loaded with
