@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define YCX_ABI_VERSION 2
+#define YCX_ABI_VERSION 3
 
 typedef int32_t ycx_status;
 enum {
@@ -51,7 +51,11 @@ enum {
   YCX_ERR_CAPACITY = 4      /* workspace / output capacity too small              */
 };
 
-enum { YCX_DT_BF16 = 0, YCX_DT_F32 = 1 };
+/* YCX_DT_FP8: OCP e4m3fn activations and weights (CDNA4 block-scaled MFMA with
+ * unit block scales, fp32 accumulate). Each activation buffer carries one
+ * power-of-two scale s (stored byte = e4m3(clamp(v * s, +-448))); weights
+ * carry one per output channel (see ycx_conv_desc). */
+enum { YCX_DT_BF16 = 0, YCX_DT_F32 = 1, YCX_DT_FP8 = 2 };
 enum { YCX_ACT_NONE = 0, YCX_ACT_SILU = 1, YCX_ACT_LEAKY = 2 };
 enum {
   YCX_OUT_NHWC = 0,       /* activation dtype, [N][Ho][Wo][out_c_stride] at out_c_off         */
@@ -61,7 +65,14 @@ enum {
 };
 
 /* Convolution: NHWC activations, weights packed [cout_pad][kh][kw][cin] in the
- * activation dtype, fp32 bias[cout_pad] (BN folded in). groups = 1. */
+ * activation dtype, fp32 bias[cout_pad] (BN folded in). groups = 1.
+ * YCX_DT_FP8: weight rows are zero-padded to a multiple of 128 bytes
+ * ([cout_pad][ceil(kh*kw*cin / 128) * 128] e4m3 of w * s_w[co]); bias points
+ * to fp32 [2 * cout_pad]: the bias, then dq[co] = 1 / (s_w[co] * s_x); the
+ * epilogue computes act(acc * dq + bias) (+ residual * res_scale) and stores
+ * e4m3(clamp(v * out_scale)) (fp32 NCHW head outputs: unscaled). The stem
+ * (ycx_stem_conv) reads the fp32 image with fp32 weights and only its output
+ * is e4m3 (out_scale). cout_pad % 64 == 0 and cin in {32, 64, 128k}. */
 typedef struct ycx_conv_desc {
   int32_t n, h, w, cin, in_c_off, in_c_stride;
   int32_t ho, wo, cout, cout_pad, out_c_off, out_c_stride;
@@ -72,9 +83,12 @@ typedef struct ycx_conv_desc {
   int32_t out_layout;       /* YCX_OUT_*                                            */
   int32_t res_c_off, res_c_stride; /* residual (same dtype/shape as the output)   */
   int32_t tile;             /* 0 = auto, else a tile id (see ycx_conv_tile_name)    */
+  float out_scale;          /* YCX_DT_FP8 only: output quantisation scale          */
+  float res_scale;          /* YCX_DT_FP8 only: residual dequantisation (1 / s_res) */
 } ycx_conv_desc;
 
-/* Max-pool, NHWC, pad value -inf (torch.nn.MaxPool2d semantics, floor mode). */
+/* Max-pool, NHWC, pad value -inf (torch.nn.MaxPool2d semantics, floor mode).
+ * YCX_DT_FP8: input and output share one scale (max commutes with it). */
 typedef struct ycx_pool_desc {
   int32_t n, h, w, c, in_c_off, in_c_stride;
   int32_t ho, wo, out_c_off, out_c_stride;
@@ -91,6 +105,7 @@ typedef struct ycx_copy_desc {
   int32_t scale;
   int32_t dtype;
   int32_t out_layout;
+  float dequant;            /* YCX_DT_FP8 with YCX_OUT_NCHW_F32: 1 / s_in (else unused) */
 } ycx_copy_desc;
 
 /* Decode of one head level (detect.py:29-87 semantics). head is fp32 NCHW
@@ -210,6 +225,9 @@ ycx_status ycx_stem_conv2(const ycx_conv_desc* stem, const ycx_conv_desc* conv, 
                           const float* b_conv, void* y, void* stream);
 ycx_status ycx_maxpool(const ycx_pool_desc* d, const void* x, void* y, void* stream);
 ycx_status ycx_copy_channels(const ycx_copy_desc* d, const void* x, void* y, void* stream);
+/* fp32 -> OCP e4m3fn bytes: y[i] = e4m3(clamp(x[i] * scale, +-448)), round to
+ * nearest even: the exact cast of the YCX_DT_FP8 epilogues (calibration checks). */
+ycx_status ycx_quantize_fp8(const float* x, void* y, int64_t n, float scale, void* stream);
 
 ycx_status ycx_decode(const ycx_decode_desc* d, const float* head, float* out, void* stream);
 /* IDetect's eval outputs for one level (nets/idetect.py:33-45): xview gets the

@@ -85,3 +85,26 @@ def test_state_dict_roundtrip_and_invalidation():
     assert m._engines == {}, "load_state_dict must drop compiled plans (packed weights)"
     for k, v in m.state_dict().items():
         assert torch.equal(v, sd[k])
+
+
+def test_fp8_weight_packing():
+    """pack_fp8_weights: per-channel power-of-two scales, exact dequantisation of
+    the e4m3 codes, rows in [kh][kw][cin] order zero-padded to 128-byte K steps."""
+    from ycx.engine import pack_fp8_weights
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(64, 32, 3, 3, generator=g, dtype=torch.float64) * torch.logspace(-3, 1, 64,
+                                                                                       dtype=torch.float64).reshape(
+        -1, 1, 1, 1)
+    w[5] = 0.0
+    q, sw = pack_fp8_weights(w)
+    assert q.dtype == torch.float8_e4m3fn and q.shape == (64, 384)  # 288 -> 3 x 128
+    assert torch.all(q[:, 288:].float() == 0)
+    assert torch.all(torch.log2(sw) == torch.round(torch.log2(sw))) and sw[5] == 1.0
+    deq = q[:, :288].double() / sw.reshape(-1, 1)
+    ref = w.permute(0, 2, 3, 1).reshape(64, -1)
+    amax = q[:, :288].float().abs().amax(1)
+    nz = torch.arange(64) != 5
+    assert torch.all((amax[nz] >= 224) & (amax[nz] <= 448))
+    # e4m3: 3 mantissa bits -> relative rounding error <= 2^-4 for normal values
+    big = ref.abs() * sw.reshape(-1, 1) >= 2 ** -6
+    assert torch.all(((deq - ref).abs() <= ref.abs() * 2 ** -4 + 1e-30)[big])

@@ -42,6 +42,7 @@ struct ConvArgs {
   int out_layout;
   int res_coff, res_cs;
   int M, HoWo, Ktot, nsteps, n_ct, nwg;
+  float out_scale, res_scale;  // YCX_DT_FP8 only
 };
 
 template <int BK>
@@ -514,6 +515,231 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
     __builtin_amdgcn_sched_barrier(0);
   }
   epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+}
+
+// -------------------------------------------------------------------------
+// fp8 (OCP e4m3fn) implicit-GEMM conv on the CDNA4 block-scaled MFMA
+// v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales (E8M0 127): twice
+// the bf16 MFMA rate, and half the HBM / LDS bytes per MAC. Same pipeline as
+// conv_bf16_glds (two-stage LDS-DMA ring, two workgroups per CU): one K step
+// is one 128-byte row per operand = 128 channels, so the LDS image, its
+// chunk swizzle and the DMA slabs are the bf16 kernel's byte for byte; a K
+// step is ONE MFMA per fragment pair (K = 128) instead of two (K = 2 x 32).
+// TPS taps per K step serve cin = 128 / TPS < 128 (64: 2 taps, 32: 4 taps):
+// lane chunk lch selects tap TPS*s + lch / (8 / TPS) and bytes 16 (lch % (8 / TPS));
+// a tap past the last fetches zeros, and the weight rows are zero-padded to a
+// multiple of 128 bytes (ycx.h), so the tail step adds exact zeros.
+// Fragments: lane l holds 32 bytes (logical chunks 2(l>>4), 2(l>>4)+1) of row
+// l&15 for A (weights) and B (pixels): the same (lane, byte) -> k map on both
+// operands, so the contraction pairs equal k whatever the hardware's k order.
+// Epilogue: v = act(acc * dq[co] + bias[co]) (+ residual * res_scale), stored
+// as e4m3(clamp(v * out_scale, +-448)) (4 bytes per lane), or fp32 NCHW heads.
+// -------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+__device__ __forceinline__ float f8_sat(float v) { return fminf(fmaxf(v, -448.0f), 448.0f); }
+
+// Four fp32 -> four e4m3fn bytes (round to nearest even, saturated first).
+__device__ __forceinline__ uint32_t f8x4_pack(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(a), f8_sat(b), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(c), f8_sat(d), w, true);
+  return (uint32_t)w;
+}
+
+// 4 consecutive fp8 output channels of pixel p (residual added first, then scaled).
+__device__ __forceinline__ void store4_f8(const ConvArgs& a, int p, int co, float v[4]) {
+  if (a.res) {
+    const int rv = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(a.res) + (size_t)p * a.res_cs +
+                                                 a.res_coff + co);
+    v[0] += __builtin_amdgcn_cvt_f32_fp8(rv, 0) * a.res_scale;
+    v[1] += __builtin_amdgcn_cvt_f32_fp8(rv, 1) * a.res_scale;
+    v[2] += __builtin_amdgcn_cvt_f32_fp8(rv, 2) * a.res_scale;
+    v[3] += __builtin_amdgcn_cvt_f32_fp8(rv, 3) * a.res_scale;
+  }
+  const float s = a.out_scale;
+  const uint32_t o = f8x4_pack(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+  uint8_t* base = reinterpret_cast<uint8_t*>(a.y) + a.out_coff + co;
+  if (a.out_layout == YCX_OUT_NHWC_UP2) {
+    const int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    const size_t W2 = 2 * (size_t)a.Wo;
+    const size_t b0 = ((size_t)n * 2 * a.Ho + 2 * oy) * W2 + 2 * ox;
+    *reinterpret_cast<uint32_t*>(base + b0 * a.out_cs) = o;
+    *reinterpret_cast<uint32_t*>(base + (b0 + 1) * a.out_cs) = o;
+    *reinterpret_cast<uint32_t*>(base + (b0 + W2) * a.out_cs) = o;
+    *reinterpret_cast<uint32_t*>(base + (b0 + W2 + 1) * a.out_cs) = o;
+  } else {
+    *reinterpret_cast<uint32_t*>(base + (size_t)p * a.out_cs) = o;
+  }
+}
+
+template <int FM, int FN>
+__device__ __forceinline__ void epilogue_f8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob, int pxb,
+                                            int lane) {
+  const float* dq = a.bias + a.Cout_pad;
+  if (a.out_layout == YCX_OUT_NCHW_F32) {
+    float* Y = reinterpret_cast<float*>(a.y);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int p = pxb + j * 16 + (lane & 15);
+        if (p >= a.M) continue;
+        const int n = p / a.HoWo, rem = p - n * a.HoWo;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = cob + i * 16 + (lane >> 4) * 4 + r;
+          if (co < a.Cout)
+            Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] =
+                ycx_act<true>(fmaf(acc[i][j][r], dq[co], a.bias[co]), a.act, a.slope);
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int co = cob + i * 16 + (lane >> 4) * 4;
+    if (co >= a.Cout) continue;  // cout % 8 == 0, co % 4 == 0: the 4 channels are all valid
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.bias + co);
+    const f32x4 qv = *reinterpret_cast<const f32x4*>(dq + co);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int p = pxb + j * 16 + (lane & 15);
+      if (p >= a.M) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = ycx_act<true>(fmaf(acc[i][j][r], qv[r], bv[r]), a.act, a.slope);
+      store4_f8(a, p, co, v);
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int TPS>
+__global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a) {
+  constexpr int NW = WM * WN, NST = 2;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(TPS == 0 || TPS == 1 || TPS == 2 || TPS == 4, "taps per K step (0: any cin % 16 == 0)");
+  constexpr int RB = 128;                   // bytes per operand row per K step
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * RB, B_BYTES = BN * RB, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_PW = BM / (8 * NW), B_PW = BN / (8 * NW);
+  constexpr int CPT = TPS ? 8 / TPS : 1;    // 16-byte chunks per tap
+  static_assert(A_PW >= 1 && B_PW >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows per wave");
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
+
+  const uint8_t* __restrict__ X = reinterpret_cast<const uint8_t*>(a.x);
+  const uint8_t* __restrict__ Wt = reinterpret_cast<const uint8_t*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
+  const int ct = L % a.n_ct, pt = L / a.n_ct;
+  const int co0 = ct * BM, px0 = pt * BN;
+  const int lrow = lane >> 3, pch = lane & 7;
+
+  const int w_bytes = a.Cout_pad * a.Ktot, x_bytes = a.N * a.H * a.W * a.in_cs;
+  int a_off[A_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int row = 8 * (wid + NW * i) + lrow;
+    a_off[i] = (co0 + row) * a.Ktot + ((pch ^ swz<64>(row)) << 4);
+  }
+  // swz<64>(row) = (4 (wid + NW i) + lrow / 2) & 7 = (4 wid + lrow / 2) & 7 for every i:
+  // the logical chunk (so the tap select) of a lane is the same in all its slabs.
+  const int lch = pch ^ swz<64>(8 * wid + lrow);
+  // TPS 0: lane chunk k = 128 s + 16 lch -> (tap, channel) = divmod(k, cin), tracked per lane
+  const int tsel = TPS == 1 ? 0 : TPS == 0 ? (16 * lch) / a.Cin : lch / CPT;
+  const int cbyte = TPS == 0 ? 0 : (TPS == 1 ? lch : lch % CPT) << 4;
+  int b_iy0[B_PW], b_ix0[B_PW], b_base[B_PW];
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int row = 8 * (wid + NW * i) + lrow;
+    const int p = px0 + row;
+    const bool ok = p < a.M;
+    const int pp = ok ? p : 0;
+    const int n = pp / a.HoWo, rem = pp - n * a.HoWo;
+    const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    b_iy0[i] = ok ? oy * a.S - a.P : -(1 << 20);  // tail rows fail the bounds test
+    b_ix0[i] = ox * a.S - a.P;
+    b_base[i] = ((n * a.H + b_iy0[i]) * a.W + b_ix0[i]) * a.in_cs + a.in_coff + cbyte;
+  }
+  // this lane's tap for the next stage to issue (TPS > 1), or the block-wide
+  // (tap, channel block) position (TPS == 1)
+  const int ntaps = a.KH * a.KW;
+  int l_tap = tsel, ky = tsel / a.KW, kx = tsel - (tsel / a.KW) * a.KW;
+  int cb = TPS == 0 ? 16 * lch - tsel * a.Cin : 0;
+  auto issue = [&](int s, int buf) {
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * RB, base + (wid + NW * i) * 1024);
+    const bool tap_ok = TPS == 1 || l_tap < ntaps;
+    const int tap = (ky * a.W + kx) * a.in_cs + cb;
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      const bool ok = tap_ok && (unsigned)(b_iy0[i] + ky) < (unsigned)a.H &&
+                      (unsigned)(b_ix0[i] + kx) < (unsigned)a.W;
+      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + A_BYTES + (wid + NW * i) * 1024);
+    }
+    if (TPS == 1) {
+      cb += RB;
+      if (cb == a.Cin) {
+        cb = 0;
+        if (++kx == a.KW) { kx = 0; ++ky; }
+      }
+    } else if (TPS == 0) {
+      cb += RB;
+      while (cb >= a.Cin) {
+        cb -= a.Cin;
+        ++l_tap;
+        if (++kx == a.KW) { kx = 0; ++ky; }
+      }
+    } else {
+      l_tap += TPS;
+      kx += TPS;
+      while (kx >= a.KW) { kx -= a.KW; ++ky; }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = a.nsteps;
+  const int c0 = 2 * (lane >> 4);
+  issue(0, 0);
+  for (int t = 0; t < nt; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < nt) issue(t + 1, (t + 1) & 1);
+    const char* A = smem + (t & 1) * STAGE;
+    const char* B = A + A_BYTES;
+    i32x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = wm * TM + i * 16 + (lane & 15);
+      const i32x4 lo = *reinterpret_cast<const i32x4*>(A + row * RB + ((c0 ^ swz<64>(row)) << 4));
+      const i32x4 hi = *reinterpret_cast<const i32x4*>(A + row * RB + (((c0 + 1) ^ swz<64>(row)) << 4));
+      af[i] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * TN + j * 16 + (lane & 15);
+      const i32x4 lo = *reinterpret_cast<const i32x4*>(B + row * RB + ((c0 ^ swz<64>(row)) << 4));
+      const i32x4 hi = *reinterpret_cast<const i32x4*>(B + row * RB + (((c0 + 1) ^ swz<64>(row)) << 4));
+      bfr[j] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  epilogue_f8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
 }
 
 // -------------------------------------------------------------------------
@@ -1169,8 +1395,15 @@ __global__ void __launch_bounds__(256) stem_kernel(ConvArgs a) {
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = ycx_act<sizeof(OutT) == 2>(v[j] + ws[wn + c0 + j], a.act, a.slope);
-    if (pv) store8<OutT>(a, p, c0, v);
+    for (int j = 0; j < 8; ++j) v[j] = ycx_act<sizeof(OutT) <= 2>(v[j] + ws[wn + c0 + j], a.act, a.slope);
+    if constexpr (sizeof(OutT) == 1) {
+      if (pv) {
+        store4_f8(a, p, c0, v);
+        store4_f8(a, p, c0 + 4, v + 4);
+      }
+    } else {
+      if (pv) store8<OutT>(a, p, c0, v);
+    }
   }
 }
 
@@ -1189,7 +1422,7 @@ __device__ __forceinline__ int stem_ch(int t, int m) {  // MFMA t, A-row m -> ou
   return 32 * (t >> 1) + 8 * (m >> 2) + 4 * (t & 1) + (m & 3);
 }
 
-template <int KH, int KW, int CIN, int CT>
+template <int KH, int KW, int CIN, int CT, bool F8 = false>  // F8: e4m3 output (x out_scale)
 __global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
   constexpr int KT = KH * KW * CIN;
   static_assert(KT <= 32 && CT % 2 == 0, "one MFMA K step, channel pairs");
@@ -1244,13 +1477,23 @@ __global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
       const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2 * q + 1], b, z, 0, 0, 0);
       const int ch0 = 32 * q + 8 * kq;
       if (ch0 < a.Cout) {
-        bf16x8 o;
+        float o[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          o[r] = (__bf16)ycx_act<true>(c0[r] + bias[2 * q][r], a.act, a.slope);
-          o[4 + r] = (__bf16)ycx_act<true>(c1[r] + bias[2 * q + 1][r], a.act, a.slope);
+          o[r] = ycx_act<true>(c0[r] + bias[2 * q][r], a.act, a.slope);
+          o[4 + r] = ycx_act<true>(c1[r] + bias[2 * q + 1][r], a.act, a.slope);
         }
-        *reinterpret_cast<bf16x8*>(Y + ((size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) * 2) = o;
+        if constexpr (F8) {
+          const float sc = a.out_scale;
+          const uint32_t lo = f8x4_pack(o[0] * sc, o[1] * sc, o[2] * sc, o[3] * sc);
+          const uint32_t hi = f8x4_pack(o[4] * sc, o[5] * sc, o[6] * sc, o[7] * sc);
+          *reinterpret_cast<uint2*>(Y + (size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) = make_uint2(lo, hi);
+        } else {
+          bf16x8 ob;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) ob[r] = (__bf16)o[r];
+          *reinterpret_cast<bf16x8*>(Y + ((size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) * 2) = ob;
+        }
       }
     }
   }
@@ -1649,7 +1892,9 @@ ConvArgs make_args(const ycx_conv_desc* d, const void* x, const void* w, const f
   a.act = d->act; a.slope = d->leaky_slope; a.out_layout = d->out_layout;
   a.res_coff = d->res_c_off; a.res_cs = d->res_c_stride;
   a.M = d->n * d->ho * d->wo; a.HoWo = d->ho * d->wo; a.Ktot = d->kh * d->kw * d->cin;
+  if (d->dtype == YCX_DT_FP8) a.Ktot = (a.Ktot + 127) / 128 * 128;  // padded weight row (bytes)
   a.nsteps = 0; a.n_ct = 0; a.nwg = 0;
+  a.out_scale = d->out_scale; a.res_scale = d->res_scale;
   return a;
 }
 
@@ -1693,6 +1938,8 @@ const TileInfo kTiles[] = {
     {128, 256, 64, "p8i_co128_px256"},
     {128, 128, 64, "glds4w_co128_px128_k64_s2"},
     {64, 128, 64, "glds4w_co64_px128_k64_s2"},
+    {128, 128, 16, "f8_co128_px128_k128_s2"},
+    {64, 128, 16, "f8_co64_px128_k128_s2"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -1744,6 +1991,26 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   a.n_ct = a.Cout_pad / BM;
   a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
   hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
+  return ycx_launch_status();
+}
+
+// fp8 tiles 34-35: cin 32 / 64 run 4 / 2 taps per 128-channel K step; other
+// cin % 16 == 0 (not 128k) walk k = (tap, channel) per lane (TPS 0).
+template <int BM, int BN, int WM, int WN>
+ycx_status launch_f8(ConvArgs a, hipStream_t st) {
+  const int tps = a.Cin == 32 ? 4 : a.Cin == 64 ? 2 : a.Cin % 128 == 0 ? 1 : 0;
+  if (tps == 0 && a.Cin % 16 != 0) return YCX_ERR_UNSUPPORTED;
+  if (a.Cout_pad % BM != 0) return YCX_ERR_UNSUPPORTED;
+  const int ntaps = a.KH * a.KW;
+  a.nsteps = (ntaps * a.Cin + 127) / 128;
+  if (a.nsteps * 128 != a.Ktot) return YCX_ERR_UNSUPPORTED;  // weight rows padded to whole K steps
+  a.n_ct = a.Cout_pad / BM;
+  a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
+  const dim3 g(a.nwg), b(WM * WN * 64);
+  if (tps == 4) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 4>), g, b, 0, st, a);
+  else if (tps == 2) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 2>), g, b, 0, st, a);
+  else if (tps == 1) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 1>), g, b, 0, st, a);
+  else hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 0>), g, b, 0, st, a);
   return ycx_launch_status();
 }
 
@@ -1803,6 +2070,8 @@ extern "C" const char* ycx_conv_tile_name(int32_t tile) {
 static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wres: no residual (tiles 22, 23)
   if (d->dtype == YCX_DT_F32) return 8;
   const long long M = (long long)d->n * d->ho * d->wo;
+  if (d->dtype == YCX_DT_FP8)
+    return d->cout_pad % 128 == 0 && (d->cout_pad / 128) * ((M + 127) / 128) >= 256 ? 34 : 35;
   const bool k64 = (d->cin % 64) == 0;
   if (d->cout_pad % 64 != 0) return 5;  // cout 32: co32 x px256, BK 32 (cin % 32 == 0)
   // The 512-thread LDS-DMA kernels' buffer descriptors address < 2 GiB per operand.
@@ -1865,11 +2134,11 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
   YCX_CHECK_ARG(d->wo == (d->w + 2 * d->pad - d->kw) / d->stride + 1);
   YCX_CHECK_ARG(d->out_c_off >= 0);
   YCX_CHECK_ARG(d->out_layout == YCX_OUT_NCHW_F32 || d->out_c_off + d->cout <= d->out_c_stride);
-  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32);
+  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
   YCX_CHECK_SUPPORTED(d->out_layout >= YCX_OUT_NHWC && d->out_layout <= YCX_OUT_NHWC_UP2);
   YCX_CHECK_SUPPORTED(d->act >= YCX_ACT_NONE && d->act <= YCX_ACT_LEAKY);
   YCX_CHECK_SUPPORTED(!residual || d->out_layout == YCX_OUT_NHWC);
-  const int vec = d->dtype == YCX_DT_BF16 ? 8 : 4;
+  const int vec = d->dtype == YCX_DT_BF16 ? 8 : d->dtype == YCX_DT_FP8 ? 16 : 4;  // 16-byte DMA chunks
   YCX_CHECK_SUPPORTED(d->in_c_off % vec == 0 && d->in_c_stride % vec == 0);
   if (d->out_layout != YCX_OUT_NCHW_F32)
     YCX_CHECK_SUPPORTED(d->cout % 8 == 0 && d->out_c_off % 8 == 0 && d->out_c_stride % 8 == 0);
@@ -1884,6 +2153,12 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
   YCX_CHECK_SUPPORTED(tile > 0 && tile < kNumTiles);
   const TileInfo& t = kTiles[tile];
   YCX_CHECK_SUPPORTED(d->cin % t.bk == 0 && d->cout_pad % t.bm == 0);
+  YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_FP8) == (tile == 34 || tile == 35));
+  if (d->dtype == YCX_DT_FP8) {
+    YCX_CHECK_SUPPORTED((long long)d->cout_pad * a.Ktot < (1LL << 31) &&
+                        (long long)d->n * d->h * d->w * d->in_c_stride < (1LL << 31) - 64);
+    return tile == 34 ? launch_f8<128, 128, 2, 4>(a, st) : launch_f8<64, 128, 1, 8>(a, st);
+  }
   if (d->dtype == YCX_DT_F32) {
     YCX_CHECK_SUPPORTED(tile == 8);
     a.nsteps = a.KH * a.KW * (a.Cin / 16);
@@ -1939,18 +2214,23 @@ extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, cons
   YCX_CHECK_SUPPORTED(d->cout % 8 == 0 && d->cout_pad % 8 == 0 && d->out_c_off % 8 == 0 &&
                       d->out_c_stride % 8 == 0 && d->out_c_off + d->cout <= d->out_c_stride);
   YCX_CHECK_SUPPORTED(d->out_layout == YCX_OUT_NHWC || d->out_layout == YCX_OUT_NHWC_UP2);
-  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32);
+  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
   YCX_CHECK_SUPPORTED((long long)d->n * d->ho * d->wo < (1LL << 31));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ConvArgs a = make_args(d, x, w, bias, y, nullptr);
-  const bool bf = d->dtype == YCX_DT_BF16;
-  if (bf && d->out_layout == YCX_OUT_NHWC && (d->cout_pad == 32 || d->cout_pad == 64) && d->wo % 16 == 0) {
+  a.Ktot = d->kh * d->kw * d->cin;  // fp32 stem weights: no fp8 row padding
+  const bool bf = d->dtype == YCX_DT_BF16, f8 = d->dtype == YCX_DT_FP8;
+  if ((bf || f8) && d->out_layout == YCX_OUT_NHWC && (d->cout_pad == 32 || d->cout_pad == 64) && d->wo % 16 == 0) {
     const long long groups = (long long)a.M / 16;
     dim3 g((unsigned)std::min<long long>((groups + 3) / 4, 256LL * 16));
 #define YCX_STEM_MFMA(KH_, KW_, CI_)                                                           \
     if (d->kh == KH_ && d->kw == KW_ && d->cin == CI_) {                                       \
-      if (d->cout_pad == 32)                                                                   \
+      if (d->cout_pad == 32 && f8)                                                             \
+        hipLaunchKernelGGL((stem_mfma<KH_, KW_, CI_, 2, true>), g, dim3(256), 0, st, a);       \
+      else if (d->cout_pad == 32)                                                              \
         hipLaunchKernelGGL((stem_mfma<KH_, KW_, CI_, 2>), g, dim3(256), 0, st, a);             \
+      else if (f8)                                                                             \
+        hipLaunchKernelGGL((stem_mfma<KH_, KW_, CI_, 4, true>), g, dim3(256), 0, st, a);       \
       else                                                                                     \
         hipLaunchKernelGGL((stem_mfma<KH_, KW_, CI_, 4>), g, dim3(256), 0, st, a);             \
       return ycx_launch_status();                                                              \
@@ -1968,6 +2248,8 @@ extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, cons
   if (d->kh == KH_ && d->kw == KW_ && d->cin == CI_) {                                           \
     if (bf)                                                                                      \
       hipLaunchKernelGGL((stem_kernel<KH_, KW_, CI_, __bf16>), grid, dim3(256), lds, st, a);     \
+    else if (f8)                                                                                 \
+      hipLaunchKernelGGL((stem_kernel<KH_, KW_, CI_, uint8_t>), grid, dim3(256), lds, st, a);    \
     else                                                                                         \
       hipLaunchKernelGGL((stem_kernel<KH_, KW_, CI_, float>), grid, dim3(256), lds, st, a);      \
     return ycx_launch_status();                                                                  \

@@ -91,6 +91,94 @@ __global__ void __launch_bounds__(256) copy_kernel(ycx_copy_desc d, const T* __r
   }
 }
 
+// ---- fp8 (OCP e4m3fn) variants: 8 channels = 8 bytes per thread ----
+__device__ __forceinline__ void f8x8_unpack(uint2 v, float f[8]) {
+  f[0] = __builtin_amdgcn_cvt_f32_fp8((int)v.x, 0); f[1] = __builtin_amdgcn_cvt_f32_fp8((int)v.x, 1);
+  f[2] = __builtin_amdgcn_cvt_f32_fp8((int)v.x, 2); f[3] = __builtin_amdgcn_cvt_f32_fp8((int)v.x, 3);
+  f[4] = __builtin_amdgcn_cvt_f32_fp8((int)v.y, 0); f[5] = __builtin_amdgcn_cvt_f32_fp8((int)v.y, 1);
+  f[6] = __builtin_amdgcn_cvt_f32_fp8((int)v.y, 2); f[7] = __builtin_amdgcn_cvt_f32_fp8((int)v.y, 3);
+}
+__device__ __forceinline__ uint32_t f8x4_pack_sat(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(a, -448.f), 448.f), fminf(fmaxf(b, -448.f), 448.f), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(c, -448.f), 448.f), fminf(fmaxf(d, -448.f), 448.f), w, true);
+  return (uint32_t)w;
+}
+
+// Max over the window in fp32 of the decoded bytes; the max is one of the
+// inputs, so re-encoding it is exact (input and output share the scale).
+__global__ void __launch_bounds__(256) maxpool_f8_kernel(ycx_pool_desc d, const uint8_t* __restrict__ x,
+                                                         uint8_t* __restrict__ y) {
+  const int cv = d.c / 8;
+  const long long total = (long long)d.n * d.ho * d.wo * cv;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % cv);
+    long long p = i / cv;
+    int ox = (int)(p % d.wo);
+    long long t = p / d.wo;
+    int oy = (int)(t % d.ho);
+    int n = (int)(t / d.ho);
+    float m[8], f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+    const int y0 = oy * d.stride - d.pad, x0 = ox * d.stride - d.pad;
+    const int ya = max(y0, 0), yb = min(y0 + d.k, d.h), xa = max(x0, 0), xb = min(x0 + d.k, d.w);
+    for (int iy = ya; iy < yb; ++iy)
+      for (int ix = xa; ix < xb; ++ix) {
+        f8x8_unpack(*reinterpret_cast<const uint2*>(x + (((size_t)n * d.h + iy) * d.w + ix) * d.in_c_stride +
+                                                    d.in_c_off + c * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+      }
+    *reinterpret_cast<uint2*>(y + (((size_t)n * d.ho + oy) * d.wo + ox) * d.out_c_stride + d.out_c_off + c * 8) =
+        make_uint2(f8x4_pack_sat(m[0], m[1], m[2], m[3]), f8x4_pack_sat(m[4], m[5], m[6], m[7]));
+  }
+}
+
+// Byte copy (same scale on both sides), or decode to fp32 NCHW x dequant.
+__global__ void __launch_bounds__(256) copy_f8_kernel(ycx_copy_desc d, const uint8_t* __restrict__ x,
+                                                      uint8_t* __restrict__ y) {
+  const int cv = d.c / 8;
+  const int ho = d.h * d.scale, wo = d.w * d.scale;
+  const long long total = (long long)d.n * ho * wo * cv;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % cv);
+    long long p = i / cv;
+    int ox = (int)(p % wo);
+    long long t = p / wo;
+    int oy = (int)(t % ho);
+    int n = (int)(t / ho);
+    int iy = oy / d.scale, ix = ox / d.scale;
+    const uint2 v = *reinterpret_cast<const uint2*>(x + (((size_t)n * d.h + iy) * d.w + ix) * d.in_c_stride +
+                                                    d.in_c_off + c * 8);
+    if (d.out_layout == YCX_OUT_NCHW_F32) {
+      float f[8];
+      f8x8_unpack(v, f);
+      float* yf = reinterpret_cast<float*>(y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        yf[(((size_t)n * d.out_c_stride + d.out_c_off + c * 8 + j) * ho + oy) * wo + ox] = f[j] * d.dequant;
+    } else {
+      *reinterpret_cast<uint2*>(y + (((size_t)n * ho + oy) * wo + ox) * d.out_c_stride + d.out_c_off + c * 8) = v;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) quantize_f8_kernel(const float* __restrict__ x, uint8_t* __restrict__ y,
+                                                          long long n, float scale) {
+  for (long long i = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * 4; i < n;
+       i += (long long)gridDim.x * blockDim.x * 4) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = i + j < n ? x[i + j] * scale : 0.0f;
+    const uint32_t w = f8x4_pack_sat(v[0], v[1], v[2], v[3]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (i + j < n) y[i + j] = (uint8_t)(w >> (8 * j));
+  }
+}
+
 unsigned grid_for(long long total) {
   long long b = (total + 255) / 256;
   if (b > 256LL * 16) b = 256LL * 16;  // grid-stride beyond 16 blocks per CU
@@ -106,13 +194,16 @@ extern "C" ycx_status ycx_maxpool(const ycx_pool_desc* d, const void* x, void* y
   YCX_CHECK_ARG(d->wo == (d->w + 2 * d->pad - d->k) / d->stride + 1);
   YCX_CHECK_ARG(d->pad * 2 <= d->k);  // torch: pad <= k/2
   YCX_CHECK_ARG(d->in_c_off + d->c <= d->in_c_stride && d->out_c_off + d->c <= d->out_c_stride);
-  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32);
-  const int vn = d->dtype == YCX_DT_BF16 ? 8 : 4;
+  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
+  const int vn = d->dtype == YCX_DT_F32 ? 4 : 8;
   YCX_CHECK_SUPPORTED(d->c % vn == 0 && d->in_c_off % vn == 0 && d->in_c_stride % vn == 0 &&
                       d->out_c_off % vn == 0 && d->out_c_stride % vn == 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   long long total = (long long)d->n * d->ho * d->wo * (d->c / vn);
-  if (d->dtype == YCX_DT_BF16)
+  if (d->dtype == YCX_DT_FP8)
+    hipLaunchKernelGGL(maxpool_f8_kernel, dim3(grid_for(total)), dim3(256), 0, st, *d, (const uint8_t*)x,
+                       (uint8_t*)y);
+  else if (d->dtype == YCX_DT_BF16)
     hipLaunchKernelGGL(maxpool_kernel<__bf16>, dim3(grid_for(total)), dim3(256), 0, st, *d,
                        (const __bf16*)x, (__bf16*)y);
   else
@@ -126,18 +217,29 @@ extern "C" ycx_status ycx_copy_channels(const ycx_copy_desc* d, const void* x, v
   YCX_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->c > 0 && (d->scale == 1 || d->scale == 2));
   YCX_CHECK_ARG(d->in_c_off + d->c <= d->in_c_stride && d->out_c_off + d->c <= d->out_c_stride);
   YCX_CHECK_SUPPORTED(d->out_layout == YCX_OUT_NHWC || d->out_layout == YCX_OUT_NCHW_F32);
-  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32);
-  const int vn = d->dtype == YCX_DT_BF16 ? 8 : 4;
+  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
+  const int vn = d->dtype == YCX_DT_F32 ? 4 : 8;
   YCX_CHECK_SUPPORTED(d->c % vn == 0 && d->in_c_off % vn == 0 && d->in_c_stride % vn == 0 &&
                       d->out_c_off % vn == 0 && d->out_c_stride % vn == 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   long long total = (long long)d->n * d->h * d->scale * d->w * d->scale * (d->c / vn);
-  if (d->dtype == YCX_DT_BF16)
+  if (d->dtype == YCX_DT_FP8)
+    hipLaunchKernelGGL(copy_f8_kernel, dim3(grid_for(total)), dim3(256), 0, st, *d, (const uint8_t*)x,
+                       (uint8_t*)y);
+  else if (d->dtype == YCX_DT_BF16)
     hipLaunchKernelGGL(copy_kernel<__bf16>, dim3(grid_for(total)), dim3(256), 0, st, *d, (const __bf16*)x,
                        (__bf16*)y);
   else
     hipLaunchKernelGGL(copy_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, *d, (const float*)x,
                        (float*)y);
+  return ycx_launch_status();
+}
+
+extern "C" ycx_status ycx_quantize_fp8(const float* x, void* y, int64_t n, float scale, void* stream) {
+  YCX_CHECK_ARG(n >= 0 && (n == 0 || (x && y)));
+  if (n == 0) return YCX_OK;
+  hipLaunchKernelGGL(quantize_f8_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), x, (uint8_t*)y, (long long)n, scale);
   return ycx_launch_status();
 }
 

@@ -18,11 +18,11 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see above)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("YCX_LIB", os.path.join(_HERE, "libycx_hip.so"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # ---- enums (ycx.h) ----
 YCX_OK, YCX_ERR_BAD_ARG, YCX_ERR_UNSUPPORTED, YCX_ERR_LAUNCH, YCX_ERR_CAPACITY = 0, 1, 2, 3, 4
-DT_BF16, DT_F32 = 0, 1
+DT_BF16, DT_F32, DT_FP8 = 0, 1, 2
 ACT_NONE, ACT_SILU, ACT_LEAKY = 0, 1, 2
 OUT_NHWC, OUT_NCHW_F32, OUT_NHWC_UP2 = 0, 1, 2
 OP_CONV, OP_STEM, OP_POOL, OP_COPY, OP_STEM2 = 1, 2, 3, 4, 5
@@ -35,7 +35,8 @@ class ConvDesc(ctypes.Structure):
         "n", "h", "w", "cin", "in_c_off", "in_c_stride",
         "ho", "wo", "cout", "cout_pad", "out_c_off", "out_c_stride",
         "kh", "kw", "stride", "pad", "act")] + [("leaky_slope", ctypes.c_float)] + [
-        (n, _i32) for n in ("dtype", "out_layout", "res_c_off", "res_c_stride", "tile")]
+        (n, _i32) for n in ("dtype", "out_layout", "res_c_off", "res_c_stride", "tile")] + [
+        ("out_scale", ctypes.c_float), ("res_scale", ctypes.c_float)]
 
 
 class PoolDesc(ctypes.Structure):
@@ -47,7 +48,7 @@ class PoolDesc(ctypes.Structure):
 class CopyDesc(ctypes.Structure):
     _fields_ = [(n, _i32) for n in (
         "n", "h", "w", "c", "in_c_off", "in_c_stride",
-        "out_c_off", "out_c_stride", "scale", "dtype", "out_layout")]
+        "out_c_off", "out_c_stride", "scale", "dtype", "out_layout")] + [("dequant", ctypes.c_float)]
 
 
 class DecodeDesc(ctypes.Structure):
@@ -116,6 +117,7 @@ _SIGS = [
                               _VP]),
     ("ycx_maxpool", _i32, [ctypes.POINTER(PoolDesc), _VP, _VP, _VP]),
     ("ycx_copy_channels", _i32, [ctypes.POINTER(CopyDesc), _VP, _VP, _VP]),
+    ("ycx_quantize_fp8", _i32, [_VP, _VP, ctypes.c_int64, ctypes.c_float, _VP]),
     ("ycx_decode", _i32, [ctypes.POINTER(DecodeDesc), _VP, _VP, _VP]),
     ("ycx_filter_decoded", _i32, [ctypes.POINTER(FilterDesc), _VP, _VP, _VP, _VP, _VP]),
     ("ycx_decode_filter", _i32, [ctypes.POINTER(DecodeFilterDesc), ctypes.POINTER(_VP), _VP, _VP, _VP, _VP]),

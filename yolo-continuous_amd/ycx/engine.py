@@ -396,23 +396,95 @@ class Plan:
                     break
 
 
+def pack_fp8_weights(wp):
+    """float64 [cout_pad][cin][k][k] -> (e4m3 [cout_pad][ceil(k*k*cin / 128) * 128] as
+    torch.float8_e4m3fn, float64 s_w[cout_pad]): per output channel the
+    power-of-two scale that maps its max |w| into [224, 448], rows in
+    [kh][kw][cin] order, zero-padded to whole 128-byte K steps (ycx.h)."""
+    cpad = wp.shape[0]
+    amax = wp.abs().amax(dim=(1, 2, 3))
+    sw = torch.where(amax > 0, torch.exp2(torch.floor(torch.log2(448.0 / amax.clamp_min(1e-300)))),
+                     torch.ones_like(amax))
+    rows = (wp * sw.reshape(-1, 1, 1, 1)).permute(0, 2, 3, 1).reshape(cpad, -1)
+    kt = rows.shape[1]
+    ktp = -(-kt // 128) * 128
+    out = torch.zeros((cpad, ktp), dtype=torch.float32)
+    out[:, :kt] = rows.to(torch.float32)
+    return out.clamp(-448.0, 448.0).to(torch.float8_e4m3fn), sw
+
+
 class Engine:
     """A compiled plan bound to device memory for one (input shape, device, precision)."""
 
-    def __init__(self, model, shape, device, precision='bf16'):
+    def __init__(self, model, shape, device, precision='bf16', fuse_stem2=True, fp8_amax=None):
         if device.type != 'cuda':
             raise RuntimeError("ycx: the HIP path needs the model input on a ROCm device (tensor.to('cuda')); "
                                "there is no CPU path")
         self.plan = Plan(model, shape)
         self.shape, self.device, self.precision = self.plan.shape, device, precision
-        self.dtype = torch.bfloat16 if precision == 'bf16' else torch.float32
-        self.dt = L.DT_BF16 if precision == 'bf16' else L.DT_F32
+        self.dtype = {'bf16': torch.bfloat16, 'f32': torch.float32, 'fp8': torch.float8_e4m3fn}[precision]
+        self.dt = {'bf16': L.DT_BF16, 'f32': L.DT_F32, 'fp8': L.DT_FP8}[precision]
+        self.fuse_stem2 = fuse_stem2
         self.graph_exec = None
         self.graph, self.out_vals, self.is_list = self.plan.graph, self.plan.out_vals, self.plan.is_list
+        self.scales = {}
+        if self.dt == L.DT_FP8:
+            if fp8_amax is None:
+                raise ValueError("ycx: an fp8 engine needs calibration amax values (Model.calibrate_fp8)")
+            self._assign_fp8_scales(fp8_amax)
         self._build()
 
-    def _cout_pad(self, cout):
+    def activation_bufs(self):
+        """The plan's activation buffers in allocation order (the order of
+        ``self.buffers``; fp8 calibration keys its amax list on it)."""
+        skip_vals = {id(nd.out) for nd in self.graph.nodes if id(nd) in self._stem2_pairs()}
+        bufs, seen = [], set()
+        for node in self.graph.nodes:
+            for v in [node.out] + node.inputs:
+                b = v.buf
+                if b is not None and id(b) not in seen and id(v) not in skip_vals:
+                    seen.add(id(b))
+                    bufs.append(b)
+        return bufs
+
+    def _assign_fp8_scales(self, amax):
+        """One power-of-two scale per group of buffers tied by a pool or a copy
+        (max-pool, nearest upsample and concat copies move bytes unchanged):
+        s = 2^floor(log2(224 / amax)), i.e. the calibrated max lands in
+        [224, 448) with 2x headroom below the e4m3 limit. Power-of-two scales
+        make every rescale exact."""
+        bufs = self.activation_bufs()
+        if len(amax) != len(bufs) or any(a.get('c') != b.c for a, b in zip(amax, bufs)):
+            raise ValueError("ycx: fp8 calibration was recorded on a different plan")
+        parent = {id(b): id(b) for b in bufs}
+
+        def find(i):
+            while parent[i] != i:
+                parent[i] = parent[parent[i]]
+                i = parent[i]
+            return i
+        for nd in self.graph.nodes:
+            if nd.kind in ('pool', 'up', 'concat'):
+                ins = [v for v in nd.inputs if v.buf is not None]
+                if nd.out.buf is None:
+                    continue
+                for v in ins:
+                    parent[find(id(v.buf))] = find(id(nd.out.buf))
+        gmax = {}
+        for a, b in zip(amax, bufs):
+            r = find(id(b))
+            gmax[r] = max(gmax.get(r, 0.0), float(a['amax']))
+        for b in bufs:
+            m = gmax[find(id(b))]
+            self.scales[id(b)] = 2.0 ** math.floor(math.log2(224.0 / m)) if m > 0 and math.isfinite(m) else 1.0
+
+    def _scale(self, v):
+        return self.scales.get(id(v.buf), 1.0) if v.buf is not None else 1.0
+
+    def _cout_pad(self, cout, stem=False):
         if self.dt == L.DT_F32:
+            return -(-cout // 64) * 64
+        if self.dt == L.DT_FP8 and not stem:
             return -(-cout // 64) * 64
         if cout <= 32:
             return 32
@@ -424,7 +496,7 @@ class Engine:
         """Stem -> 3x3/s2 conv pairs that run as one ycx_stem_conv2 (the stem
         map stays in LDS): bf16, the stem's output read by that conv only."""
         pairs = {}
-        if self.dt != L.DT_BF16:
+        if self.dt != L.DT_BF16 or not self.fuse_stem2:
             return pairs
         for nd in self.graph.nodes:
             if nd.kind != 'stem':
@@ -452,15 +524,9 @@ class Engine:
         self.buffers, self.params = [], []
         pairs = self._stem2_pairs()
         fused = {id(c) for c in pairs.values()}
-        skip_vals = {id(nd.out) for nd in self.graph.nodes if id(nd) in pairs}  # stem maps that stay in LDS
-        seen = set()
-        for node in self.graph.nodes:
-            for v in [node.out] + node.inputs:
-                b = v.buf
-                if b is not None and id(b) not in seen and id(v) not in skip_vals:
-                    seen.add(id(b))
-                    b.tensor = torch.empty((b.n, b.h, b.w, b.c), dtype=dt, device=dev)
-                    self.buffers.append(b.tensor)
+        for b in self.activation_bufs():  # the stem maps of fused stem2 pairs stay in LDS
+            b.tensor = torch.empty((b.n, b.h, b.w, b.c), dtype=dt, device=dev)
+            self.buffers.append(b.tensor)
         ops, self.input_slots, self.output_slots, self.op_info = [], [], {}, []
         self.conv_flops = 0
         for node in self.graph.nodes:
@@ -503,13 +569,18 @@ class Engine:
         w64, b64 = p['w'], p['b']
         cout, cin, k = int(w64.shape[0]), int(w64.shape[1]), p['k']
         stem = node.kind == 'stem'
-        cpad = self._cout_pad(cout)
+        cpad = self._cout_pad(cout, stem)
         wp = torch.zeros((cpad, cin, k, k), dtype=torch.float64)
         wp[:cout] = w64
         bp = torch.zeros(cpad, dtype=torch.float64)
         bp[:cout] = b64
+        f8 = self.dt == L.DT_FP8
         if stem:  # [kh][kw][cin][cout_pad] fp32
             wt = wp.permute(2, 3, 1, 0).contiguous().to(torch.float32)
+        elif f8:  # e4m3 rows of w * s_w[co], [cout_pad][kh*kw*cin padded to 128 B]
+            wt, sw = pack_fp8_weights(wp)
+            dq = 1.0 / (sw * self._scale(x))
+            bp = torch.cat([bp, dq])
         else:     # [cout_pad][kh][kw][cin] in the activation dtype
             wt = wp.permute(0, 2, 3, 1).contiguous().to(self.dtype)
         wt = wt.to(self.device)
@@ -533,6 +604,8 @@ class Engine:
         if r is not None:
             d.res_c_off, d.res_c_stride = r.coff, r.buf.c
         d.tile = 0
+        d.out_scale = self._scale(out) if (f8 and p['layout'] != L.OUT_NCHW_F32) else 1.0
+        d.res_scale = 1.0 / self._scale(r) if (f8 and r is not None) else 1.0
         flops = 2 * x.n * p['ho'] * p['wo'] * cout * cin * k * k
         self.conv_flops += flops
         return d, wt, bt, flops, (x.n, x.h, x.w, cin, cout, k, p['s'])
@@ -590,6 +663,7 @@ class Engine:
         op.kind = L.OP_COPY
         idx = len(self.op_info)
         op.in_ = x.buf.tensor.data_ptr()
+        d.dequant = 1.0 / self._scale(x) if self.dt == L.DT_FP8 else 1.0
         if nchw:
             d.out_c_off, d.out_c_stride, d.out_layout = 0, x.c, L.OUT_NCHW_F32
             op.out = self._val_ptr(out, idx, 'out')

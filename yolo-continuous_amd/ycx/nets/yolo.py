@@ -133,7 +133,7 @@ class WeightInitial(Enum):
     Random = 1
 
 
-PRECISIONS = ('bf16', 'f32')
+PRECISIONS = ('bf16', 'f32', 'fp8')
 
 
 class Model(nn.Module):
@@ -142,7 +142,9 @@ class Model(nn.Module):
     forward(x: fp32 [N, C, H, W] on a ROCm device) -> the last layer's output:
     ``[P5, P4, P3]`` fp32 NCHW logits for a Detect head (nets/detect.py:38).
     ``precision`` selects the kernel dtype: 'bf16' (default, MFMA bf16, fp32
-    accumulate) or 'f32' (parity mode, exact-fp32 MFMA).
+    accumulate), 'f32' (parity mode, exact-fp32 MFMA) or 'fp8' (OCP e4m3
+    weights and activations on the block-scaled MFMA, fp32 accumulate; the
+    activation scales come from ``calibrate_fp8``).
     """
 
     def __init__(self, model_cfg, anchors, num_classes, image_chan=3, weight_initial=WeightInitial.Random,
@@ -171,7 +173,7 @@ class Model(nn.Module):
                 nn.init.constant_(m.bias, 0)
             elif isinstance(m, (nn.Hardswish, nn.LeakyReLU, nn.ReLU, nn.ReLU6)):
                 m.inplace = True
-        self.invalidate()
+        self.invalidate(weights_changed=True)
 
     def print_info(self):
         n_p = sum(x.numel() for x in self.parameters())
@@ -202,11 +204,14 @@ class Model(nn.Module):
         self.invalidate()
         return self
 
-    def invalidate(self):
-        """Drop compiled plans (packed weights); called when parameters change."""
+    def invalidate(self, weights_changed=False):
+        """Drop compiled plans (packed weights); called when parameters change
+        (then the fp8 calibration records are stale too)."""
         for eng in getattr(self, '_engines', {}).values():
             eng.close()
         self._engines = {}
+        if weights_changed or not hasattr(self, '_fp8_amax'):
+            self._fp8_amax = {}  # (H, W) -> calibration record
 
     def engine_for(self, shape, device, slot=0):
         """The compiled plan for (shape, device, precision); ``slot`` > 0 gives an
@@ -217,13 +222,44 @@ class Model(nn.Module):
         key = (shape, str(dev), self.precision, int(slot))
         eng = self._engines.get(key)
         if eng is None:
-            eng = Engine(self, shape, dev, self.precision)
+            amax = None
+            if self.precision == 'fp8':
+                amax = self._fp8_amax.get(shape[2:])
+                if amax is None:
+                    amax = self.calibrate_fp8(device=dev, hw=shape[2:])
+            eng = Engine(self, shape, dev, self.precision, fp8_amax=amax)
             self._engines[key] = eng
         return eng
 
+    def calibrate_fp8(self, images=None, device=None, hw=None, n=4, seed=0):
+        """fp8 activation calibration: one bf16 forward over ``images`` (fp32
+        [N, C, H, W]) records max |activation| per buffer of the plan; every fp8
+        engine for that (H, W) derives its power-of-two scales from it. Without
+        images a seeded synthetic U[0,1) batch of ``n`` images at ``hw`` is used
+        (no calibration set ships with the reference). Returns the record."""
+        from ..engine import Engine
+        from ..utils.synth import synthetic_images
+        if images is None:
+            if hw is None:
+                raise ValueError("ycx: calibrate_fp8 needs images or hw=(H, W)")
+            images = synthetic_images(n, self.image_chan, int(hw[0]), int(hw[1]), seed=seed)
+        dev = torch.device(device) if device is not None else images.device
+        images = images.to(dev, torch.float32).contiguous()
+        eng = Engine(self, tuple(images.shape), dev, 'bf16', fuse_stem2=False)
+        try:
+            eng.run(images)
+            amax = [dict(c=int(b.c), amax=float(b.tensor.abs().max().float())) for b in eng.activation_bufs()]
+        finally:
+            eng.close()
+        key = tuple(int(v) for v in images.shape[2:])
+        self._fp8_amax[key] = amax
+        for k in [k for k in self._engines if k[2] == 'fp8' and k[0][2:] == key]:
+            self._engines.pop(k).close()
+        return amax
+
     def load_state_dict(self, state_dict, strict=True, *args, **kwargs):
         r = super().load_state_dict(state_dict, strict, *args, **kwargs)
-        self.invalidate()
+        self.invalidate(weights_changed=True)
         return r
 
     def _apply(self, fn, *args, **kwargs):
