@@ -219,7 +219,9 @@ ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, const float* w,
  * consumes only it: one kernel, the 32-channel stem map never reaches HBM.
  * `stem` and `conv` are the two layers' own descriptors (conv->h/w = the stem
  * output size); conv output as for ycx_conv2d (NHWC bf16, channel slice).
- * Requires conv->ho % 4 == 0, conv->wo % 32 == 0 and stem->act == conv->act. */
+ * Requires conv->ho % 4 == 0, conv->wo % 32 == 0 and stem->act == conv->act.
+ * dtype YCX_DT_FP8 (both descriptors): the pair still computes in bf16 with
+ * bf16 w_conv and plain bias; only the output is e4m3 (conv->out_scale). */
 ycx_status ycx_stem_conv2(const ycx_conv_desc* stem, const ycx_conv_desc* conv, const float* x,
                           const float* w_stem, const float* b_stem, const void* w_conv,
                           const float* b_conv, void* y, void* stream);

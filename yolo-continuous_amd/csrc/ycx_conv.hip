@@ -1537,7 +1537,7 @@ __device__ __forceinline__ int s2_swz(int col) { return (col ^ ((col >> 1) & 2))
 
 constexpr int s2_pad(int v, int m) { return v + ((m - v % 32) + 32) % 32; }  // smallest >= v, == m mod 32
 
-template <int SS, int ACT1, int ACT2>  // stem stride, stem / conv activation
+template <int SS, int ACT1, int ACT2, bool F8 = false>  // stem stride, stem / conv act, e4m3 output
 __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) {
   constexpr int NPIX = kS2R * kS2C, NGRP = (NPIX + 15) / 16, GPW = (NGRP + 3) / 4;
   constexpr int IR = (kS2R - 1) * SS + 3, IC = (kS2C - 1) * SS + 3;  // image patch rows / cols
@@ -1720,10 +1720,17 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int p = n * ca.HoWo + (oy0 + 2 * wn + (j >> 1)) * ca.Wo + ox0 + 16 * (j & 1) + lx;
-        bf16x4 ov;
+        if constexpr (F8) {  // the stem map and this conv run in bf16; only the output is e4m3
+          const float sc = ca.out_scale;
+          *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ca.y) + ca.out_coff + (size_t)p * ca.out_cs + co) =
+              f8x4_pack(act_t<ACT2>(acc[i][j][0], ca.slope) * sc, act_t<ACT2>(acc[i][j][1], ca.slope) * sc,
+                        act_t<ACT2>(acc[i][j][2], ca.slope) * sc, act_t<ACT2>(acc[i][j][3], ca.slope) * sc);
+        } else {
+          bf16x4 ov;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ov[q] = (__bf16)act_t<ACT2>(acc[i][j][q], ca.slope);
-        *reinterpret_cast<bf16x4*>(Y + (size_t)p * ca.out_cs + co) = ov;
+          for (int q = 0; q < 4; ++q) ov[q] = (__bf16)act_t<ACT2>(acc[i][j][q], ca.slope);
+          *reinterpret_cast<bf16x4*>(Y + (size_t)p * ca.out_cs + co) = ov;
+        }
       }
     }
   }
@@ -2280,20 +2287,29 @@ extern "C" ycx_status ycx_stem_conv2(const ycx_conv_desc* sd, const ycx_conv_des
                       sd->cin == 3 && sd->cout == 32 && sd->cout_pad == 32);
   YCX_CHECK_SUPPORTED(cd->kh == 3 && cd->kw == 3 && cd->stride == 2 && cd->pad == 1 && cd->cin == 32 &&
                       cd->cout_pad == 64 && cd->cout % 8 == 0 && cd->out_c_off % 8 == 0 && cd->out_c_stride % 8 == 0);
-  YCX_CHECK_SUPPORTED(sd->dtype == YCX_DT_BF16 && cd->dtype == YCX_DT_BF16 && cd->out_layout == YCX_OUT_NHWC);
+  // FP8: the pair computes in bf16 (the stem map never leaves LDS); the output is e4m3 (cd->out_scale)
+  YCX_CHECK_SUPPORTED(sd->dtype == cd->dtype && (cd->dtype == YCX_DT_BF16 || cd->dtype == YCX_DT_FP8) &&
+                      cd->out_layout == YCX_OUT_NHWC);
   YCX_CHECK_SUPPORTED(sd->act >= YCX_ACT_NONE && sd->act <= YCX_ACT_LEAKY && cd->act >= YCX_ACT_NONE &&
                       cd->act <= YCX_ACT_LEAKY);
   YCX_CHECK_SUPPORTED(cd->ho % kS2TH == 0 && cd->wo % kS2TW == 0);
   YCX_CHECK_SUPPORTED((long long)cd->n * cd->ho * cd->wo < (1LL << 31));
   ConvArgs sa = make_args(sd, x, w_stem, b_stem, nullptr, nullptr);
   ConvArgs ca = make_args(cd, nullptr, w_conv, b_conv, y, nullptr);
+  const bool f8 = cd->dtype == YCX_DT_FP8;
+  // both weight sets are unpadded (fp32 stem, bf16 conv) whatever the output dtype
+  sa.Ktot = sd->kh * sd->kw * sd->cin;
+  ca.Ktot = cd->kh * cd->kw * cd->cin;
   const long long ntiles = (long long)cd->n * (cd->ho / kS2TH) * (cd->wo / kS2TW);
   ca.nwg = (int)std::min<long long>(ntiles, 2 * 256);  // persistent: two blocks per CU
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 g(ca.nwg), b(256);
 #define YCX_STEM2(SS_, A1_, A2_)                                                           \
   if (sd->stride == SS_ && sd->act == A1_ && cd->act == A2_) {                            \
-    hipLaunchKernelGGL((stem2_fused<SS_, A1_, A2_>), g, b, 0, st, sa, ca);                \
+    if (f8)                                                                               \
+      hipLaunchKernelGGL((stem2_fused<SS_, A1_, A2_, true>), g, b, 0, st, sa, ca);        \
+    else                                                                                  \
+      hipLaunchKernelGGL((stem2_fused<SS_, A1_, A2_>), g, b, 0, st, sa, ca);              \
     return ycx_launch_status();                                                           \
   }
   YCX_STEM2(1, YCX_ACT_SILU, YCX_ACT_SILU)

@@ -496,7 +496,7 @@ class Engine:
         """Stem -> 3x3/s2 conv pairs that run as one ycx_stem_conv2 (the stem
         map stays in LDS): bf16, the stem's output read by that conv only."""
         pairs = {}
-        if self.dt != L.DT_BF16 or not self.fuse_stem2:
+        if self.dt not in (L.DT_BF16, L.DT_FP8) or not self.fuse_stem2:
             return pairs
         for nd in self.graph.nodes:
             if nd.kind != 'stem':
@@ -563,13 +563,14 @@ class Engine:
             return None
         return v.buf.tensor.data_ptr()
 
-    def _conv_parts(self, node):
-        """Packed weights/bias (kept alive in self.params) and the descriptor of a conv/stem node."""
+    def _conv_parts(self, node, bf16_weights=False):
+        """Packed weights/bias (kept alive in self.params) and the descriptor of a conv/stem node.
+        bf16_weights: bf16 packing whatever the plan dtype (the fp8 stem2 pair computes in bf16)."""
         p, x, out = node.p, node.inputs[0], node.out
         w64, b64 = p['w'], p['b']
         cout, cin, k = int(w64.shape[0]), int(w64.shape[1]), p['k']
         stem = node.kind == 'stem'
-        cpad = self._cout_pad(cout, stem)
+        cpad = self._cout_pad(cout, stem or bf16_weights)
         wp = torch.zeros((cpad, cin, k, k), dtype=torch.float64)
         wp[:cout] = w64
         bp = torch.zeros(cpad, dtype=torch.float64)
@@ -577,6 +578,8 @@ class Engine:
         f8 = self.dt == L.DT_FP8
         if stem:  # [kh][kw][cin][cout_pad] fp32
             wt = wp.permute(2, 3, 1, 0).contiguous().to(torch.float32)
+        elif bf16_weights:
+            wt = wp.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
         elif f8:  # e4m3 rows of w * s_w[co], [cout_pad][kh*kw*cin padded to 128 B]
             wt, sw = pack_fp8_weights(wp)
             dq = 1.0 / (sw * self._scale(x))
@@ -629,7 +632,7 @@ class Engine:
 
     def _stem2_op(self, stem, conv):
         ds, ws, bs, fs, _ = self._conv_parts(stem)
-        dc, wc, bc, fc, shape = self._conv_parts(conv)
+        dc, wc, bc, fc, shape = self._conv_parts(conv, bf16_weights=True)
         op = L.Op()
         op.kind = L.OP_STEM2
         op.d.pair[0], op.d.pair[1] = ds, dc
