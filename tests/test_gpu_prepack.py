@@ -1,0 +1,42 @@
+"""ycx.prepack: folded + packed weights (and the fp8 calibration)
+round-trip through a safetensors file; a model that loads them reproduces the
+packing model's outputs bit for bit without folding its own parameters."""
+import pytest
+import torch
+
+from helpers import make_model
+from ycx.utils.synth import synthetic_images
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('precision', ['bf16', 'fp8', 'f32'])
+def test_prepack_roundtrip_bit_exact(device, tmp_path, precision):
+    src, _ = make_model('yolov7-tiny', 1, 0, precision)
+    src.to(device)
+    x = synthetic_images(2, 3, 320, 320, seed=4).to(device)
+    ref = [o.clone() for o in src(x)]
+    path = str(tmp_path / f"tiny_{precision}.safetensors")
+    meta = src.save_prepacked(path, (320, 320))
+    assert meta['precision'] == precision and meta['hw'] == [320, 320]
+    dst, _ = make_model('yolov7-tiny', 1, 7, 'bf16')  # other weights: the file must win
+    with pytest.raises(ValueError, match='different state_dict'):
+        dst.load_prepacked(path, strict=True)
+    dst.load_prepacked(path)
+    assert dst.precision == precision
+    dst.to(device)
+    out = dst(x)
+    for a, b in zip(out, ref):
+        assert torch.equal(a, b)
+
+
+def test_prepack_rejects_other_plan(device, tmp_path):
+    src, _ = make_model('yolov7-tiny', 1, 0, 'bf16')
+    src.to(device)
+    path = str(tmp_path / "tiny.safetensors")
+    src.save_prepacked(path, (320, 320))
+    other, _ = make_model('yolov7', 80, 0, 'bf16')
+    other.load_prepacked(path)
+    other.to(device)
+    with pytest.raises(ValueError, match='do not match this plan'):
+        other(torch.zeros(1, 3, 320, 320, device=device))

@@ -108,3 +108,19 @@ def test_fp8_weight_packing():
     # e4m3: 3 mantissa bits -> relative rounding error <= 2^-4 for normal values
     big = ref.abs() * sw.reshape(-1, 1) >= 2 ** -6
     assert torch.all(((deq - ref).abs() <= ref.abs() * 2 ** -4 + 1e-30)[big])
+
+
+def test_prepack_file_format_checks(tmp_path):
+    """ycx.prepack.load refuses files that are not ycx prepack files (CPU: format only)."""
+    from safetensors.torch import save_file
+    from ycx import prepack
+    p = str(tmp_path / "plain.safetensors")
+    save_file({"a": torch.zeros(2)}, p)
+    with pytest.raises(ValueError, match="not a ycx prepack file"):
+        prepack.load(p)
+    save_file({"p0": torch.zeros(2)}, p, metadata={"ycx": '{"format": "other"}'})
+    with pytest.raises(ValueError, match="format"):
+        prepack.load(p)
+    m, _ = make_model('yolov7-tiny', 1, 0)
+    h = prepack.state_dict_sha256(m)
+    assert h == prepack.state_dict_sha256(m) and len(h) == 64

@@ -416,7 +416,7 @@ def pack_fp8_weights(wp):
 class Engine:
     """A compiled plan bound to device memory for one (input shape, device, precision)."""
 
-    def __init__(self, model, shape, device, precision='bf16', fuse_stem2=True, fp8_amax=None):
+    def __init__(self, model, shape, device, precision='bf16', fuse_stem2=True, fp8_amax=None, prepacked=None):
         if device.type != 'cuda':
             raise RuntimeError("ycx: the HIP path needs the model input on a ROCm device (tensor.to('cuda')); "
                                "there is no CPU path")
@@ -425,6 +425,7 @@ class Engine:
         self.dtype = {'bf16': torch.bfloat16, 'f32': torch.float32, 'fp8': torch.float8_e4m3fn}[precision]
         self.dt = {'bf16': L.DT_BF16, 'f32': L.DT_F32, 'fp8': L.DT_FP8}[precision]
         self.fuse_stem2 = fuse_stem2
+        self.prepacked = prepacked  # {'p<i>': packed tensor} from ycx.prepack (skips folding / packing)
         self.graph_exec = None
         self.graph, self.out_vals, self.is_list = self.plan.graph, self.plan.out_vals, self.plan.is_list
         self.scales = {}
@@ -571,23 +572,39 @@ class Engine:
         cout, cin, k = int(w64.shape[0]), int(w64.shape[1]), p['k']
         stem = node.kind == 'stem'
         cpad = self._cout_pad(cout, stem or bf16_weights)
-        wp = torch.zeros((cpad, cin, k, k), dtype=torch.float64)
-        wp[:cout] = w64
-        bp = torch.zeros(cpad, dtype=torch.float64)
-        bp[:cout] = b64
         f8 = self.dt == L.DT_FP8
         if stem:  # [kh][kw][cin][cout_pad] fp32
-            wt = wp.permute(2, 3, 1, 0).contiguous().to(torch.float32)
+            wshape, wdt = (k, k, cin, cpad), torch.float32
         elif bf16_weights:
-            wt = wp.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+            wshape, wdt = (cpad, k, k, cin), torch.bfloat16
         elif f8:  # e4m3 rows of w * s_w[co], [cout_pad][kh*kw*cin padded to 128 B]
-            wt, sw = pack_fp8_weights(wp)
-            dq = 1.0 / (sw * self._scale(x))
-            bp = torch.cat([bp, dq])
+            wshape, wdt = (cpad, -(-k * k * cin // 128) * 128), torch.float8_e4m3fn
         else:     # [cout_pad][kh][kw][cin] in the activation dtype
-            wt = wp.permute(0, 2, 3, 1).contiguous().to(self.dtype)
+            wshape, wdt = (cpad, k, k, cin), self.dtype
+        bshape = (2 * cpad,) if (f8 and not stem and not bf16_weights) else (cpad,)
+        if self.prepacked is not None:
+            i = len(self.params)
+            wt, bt = self.prepacked.get(f"p{i}"), self.prepacked.get(f"p{i + 1}")
+            if wt is None or bt is None or tuple(wt.shape) != wshape or wt.dtype != wdt or \
+                    tuple(bt.shape) != bshape or bt.dtype != torch.float32:
+                raise ValueError(f"ycx: prepacked weights do not match this plan at tensor p{i}")
+        else:
+            wp = torch.zeros((cpad, cin, k, k), dtype=torch.float64)
+            wp[:cout] = w64
+            bp = torch.zeros(cpad, dtype=torch.float64)
+            bp[:cout] = b64
+            if stem:
+                wt = wp.permute(2, 3, 1, 0).contiguous().to(torch.float32)
+            elif bf16_weights:
+                wt = wp.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+            elif f8:
+                wt, sw = pack_fp8_weights(wp)
+                bp = torch.cat([bp, 1.0 / (sw * self._scale(x))])  # dq[co] = 1 / (s_w[co] s_x)
+            else:
+                wt = wp.permute(0, 2, 3, 1).contiguous().to(self.dtype)
+            bt = bp.to(torch.float32)
         wt = wt.to(self.device)
-        bt = bp.to(torch.float32).to(self.device)
+        bt = bt.to(self.device)
         self.params += [wt, bt]
         d = L.ConvDesc()
         d.n, d.h, d.w, d.cin = x.n, x.h, x.w, cin

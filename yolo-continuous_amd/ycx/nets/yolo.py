@@ -212,6 +212,7 @@ class Model(nn.Module):
         self._engines = {}
         if weights_changed or not hasattr(self, '_fp8_amax'):
             self._fp8_amax = {}  # (H, W) -> calibration record
+            self._prepacked = {}  # (precision, H, W) -> packed tensors (ycx.prepack)
 
     def engine_for(self, shape, device, slot=0):
         """The compiled plan for (shape, device, precision); ``slot`` > 0 gives an
@@ -227,7 +228,8 @@ class Model(nn.Module):
                 amax = self._fp8_amax.get(shape[2:])
                 if amax is None:
                     amax = self.calibrate_fp8(device=dev, hw=shape[2:])
-            eng = Engine(self, shape, dev, self.precision, fp8_amax=amax)
+            eng = Engine(self, shape, dev, self.precision, fp8_amax=amax,
+                         prepacked=self._prepacked.get((self.precision,) + shape[2:]))
             self._engines[key] = eng
         return eng
 
@@ -256,6 +258,28 @@ class Model(nn.Module):
         for k in [k for k in self._engines if k[2] == 'fp8' and k[0][2:] == key]:
             self._engines.pop(k).close()
         return amax
+
+    def save_prepacked(self, path, hw, precision=None, device='cuda'):
+        """Write the folded, packed weights of the (precision, H, W) plan (and its
+        fp8 calibration) to a safetensors file (ycx.prepack)."""
+        from .. import prepack
+        return prepack.save(self, path, hw, precision, device)
+
+    def load_prepacked(self, path, strict=False):
+        """Use the packed weights of a ycx.prepack file for its (precision, H, W)
+        plan instead of folding this module's parameters, and switch to its
+        precision. strict: the file must come from this module's current
+        state_dict."""
+        from .. import prepack
+        meta, tensors = prepack.load(path)
+        if strict and meta.get('state_dict_sha256') != prepack.state_dict_sha256(self):
+            raise ValueError(f"ycx: {path} was packed from a different state_dict")
+        hw = tuple(meta['hw'])
+        self.set_precision(meta['precision'])
+        self._prepacked[(meta['precision'],) + hw] = tensors
+        if meta['precision'] == 'fp8':
+            self._fp8_amax[hw] = meta['fp8_amax']
+        return meta
 
     def load_state_dict(self, state_dict, strict=True, *args, **kwargs):
         r = super().load_state_dict(state_dict, strict, *args, **kwargs)
