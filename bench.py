@@ -58,6 +58,10 @@ def parse(argv=None):
     ap.add_argument("--max-det", type=int, default=300)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample (0: skip)")
     ap.add_argument("--roofline-steps", type=int, default=3)
+    ap.add_argument("--dist", action="store_true",
+                    help="run the N > 1 code path (process group + RCCL all-gather) even at one rank")
+    ap.add_argument("--latency-steps", type=int, default=10,
+                    help="unloaded latency leg: batches run one at a time (0: skip)")
     return ap.parse_args(argv)
 
 
@@ -192,38 +196,38 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    dist_on = world > 1 or args.dist  # --dist: the N > 1 code path (RCCL gather) on a single rank
+    if dist_on:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
     mode = "serial" if args.no_pipeline else args.mode
     pipeline = False if mode == "serial" else mode
     model, det, sd, cfg, shape = setup(args, dev, rank, pipeline=pipeline)
     from ycx.dist import gather_detections
-    s_coll = torch.cuda.Stream(dev) if (world > 1 and mode == "concurrent") else None
     lat_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
 
+    def gather(dets, keep, kc):  # the single collective: all-gather of padded detections (+ counts, keep rows)
+        g_dets, g_kc, g_keep = gather_detections(dets, kc, keep)
+        return g_dets, g_keep, g_kc
+
     def step(i=None):
         timing = lat_ev[i] if i is not None else None
-        if mode == "concurrent":
-            dets, keep, kc, done = det.submit(timing=(timing[0], None) if (timing and world > 1) else timing)
-            if world > 1:  # the single collective, in batch order on one stream (same order on every rank)
-                with torch.cuda.stream(s_coll):
-                    s_coll.wait_event(done)
-                    dets, kc, keep = gather_detections(dets, kc, keep)
-                    if timing is not None:
-                        timing[1].record(s_coll)
+        if mode == "concurrent":  # the collective on the batch's own stream, issued in batch order on every rank
+            dets, keep, kc, done = det.submit(timing=timing, then=gather if dist_on else None)
             return kc
         if pipeline:
             dets, keep, kc, _ = det.submit(timing=timing)
-            if world > 1:  # the single collective, on the post stream after this batch's NMS
+            if dist_on:  # the single collective, on the post stream after this batch's NMS
                 with torch.cuda.stream(det.s_post):
                     dets, kc, keep = gather_detections(dets, kc, keep)
             return kc
         if timing is not None:
             timing[0].record()
         dets, keep, kc = det()
-        if world > 1:  # the single collective: all-gather of padded detections (+ counts, keep rows)
+        if dist_on:  # the single collective: all-gather of padded detections (+ counts, keep rows)
             dets, kc, keep = gather_detections(dets, kc, keep)
         if timing is not None:
             timing[1].record()
@@ -232,26 +236,34 @@ def main():
     def drain():
         if pipeline:
             det.synchronize()
-        if s_coll is not None:
-            torch.cuda.current_stream().wait_stream(s_coll)
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step()
     drain()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         kc = step(i)
     drain()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     lat = [a.elapsed_time(b) for a, b in lat_ev]
+    # unloaded latency: one batch in flight at a time (input resident -> detections, + gather)
+    lat1 = []
+    for _ in range(args.latency_steps):
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        step()
+        drain()
+        lat1.append((time.perf_counter() - t1) * 1e3)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     images = world * args.batch * args.steps
@@ -268,6 +280,7 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "p50_ms": round(statistics.median(lat), 4), "p90_ms": round(sorted(lat)[int(0.9 * (len(lat) - 1))], 4),
+            "p50_ms_unloaded": round(statistics.median(lat1), 4) if lat1 else None,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic U[0,1) images, seeded synthetic weights (no checkpoint exists)",
             "config": {"workload": f"{args.net} COCO-{args.nc} {args.size}x{args.size}, {args.batch} images per GPU "
@@ -276,6 +289,8 @@ def main():
                        "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
                        "mode": mode, "batches_in_flight": (args.depth if mode == "concurrent" else
                                                            2 if mode == "pipelined" else 1),
+                       "latency": "p50_ms: submit -> detections of a batch in the timed loop (batches_in_flight "
+                                  "queued); p50_ms_unloaded: host wall time of one batch alone, synchronised",
                        "conf_thres": args.conf, "iou_thres": args.iou, "max_det": args.max_det},
             "mfma_fraction_whole_step": round(model.engine_for(shape, dev).flops_per_image * value /
                                               (world * peak * 1e12), 4),
@@ -293,7 +308,7 @@ def main():
         if os.environ.get("YCX_BENCH_KERNELS"):
             with open(os.environ["YCX_BENCH_KERNELS"], "w") as f:
                 json.dump(dict(per_kernel=rl['per_kernel'], ops=rl['ops']), f, indent=1)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -1888,6 +1888,139 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
   }
 }
 
+// -------------------------------------------------------------------------
+// fp8 weight-resident 1x1 conv (tile 36): conv1x1_wres's structure on the
+// block-scaled e4m3 MFMA. Wave (wc, wp) holds the e4m3 rows of output channels
+// 32 wc .. +31 of its group for all of K in registers (K/4 VGPRs: 64 at
+// cin 512) and streams PT-pixel tiles of activations HBM -> LDS once each
+// through an NS-stage LDS-DMA ring of 128-channel slabs (PT rows x 128 B,
+// XOR-swizzled as in conv_f8_glds); one ring step = one 16x16x128 MFMA per
+// fragment pair. The ring runs across tiles: a full tile's epilogue issues
+// exactly FM x FN dword stores per wave, counted into the next waits.
+// Requires 1x1/s1/p0, cin = 128 KC (KC = 1, 2, 4), NHWC e4m3 output without residual.
+// -------------------------------------------------------------------------
+template <int WCO, int WPX, int TPW, int KC, int NS>
+__global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
+  constexpr int NW = WCO * WPX, PT = TPW * WPX, FM = 2, FN = TPW / 16, BCO = WCO * 32;
+  constexpr int STAGE = PT * 128, A_PW = PT / (8 * NW);
+  constexpr int NSTO = FM * FN;  // dword stores per wave per tile
+  constexpr int VM_RING = A_PW * (NS - 2);
+  static_assert(A_PW >= 1 && PT % (8 * NW) == 0 && TPW % 16 == 0, "tile rows per wave");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wc = wid % WCO, wp = wid / WCO;
+  const int G = a.n_ct;
+  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
+  const int g = L % G, r = L / G, R = a.nwg / G;
+  const int T = (a.M + PT - 1) / PT;
+  const int t0 = (int)((long long)r * T / R), t1 = (int)((long long)(r + 1) * T / R);
+  if (t0 >= t1) return;  // whole block: no barrier is left waiting
+  const int cob = g * BCO + wc * 32;
+  const int c0 = 2 * (lane >> 4);
+
+  // this wave's weights: A fragment (slab s, i) = bytes 128 s + 16 c0 .. +31 of row cob + 16 i + (lane & 15)
+  const uint8_t* __restrict__ Wt = reinterpret_cast<const uint8_t*>(a.w);
+  i32x8 af[KC][FM];
+#pragma unroll
+  for (int s = 0; s < KC; ++s)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const uint8_t* w = Wt + (size_t)(cob + 16 * i + (lane & 15)) * a.Ktot + 128 * s + 16 * c0;
+      const i32x4 lo = *reinterpret_cast<const i32x4*>(w), hi = *reinterpret_cast<const i32x4*>(w + 16);
+      af[s][i] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  f32x4 bv[FM], qv[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int co = cob + 16 * i + 4 * (lane >> 4);
+    const bool ok = co < a.Cout;
+    bv[i] = ok ? *reinterpret_cast<const f32x4*>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+    qv[i] = ok ? *reinterpret_cast<const f32x4*>(a.bias + a.Cout_pad + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // LDS-DMA: wave-instruction (wid + NW i) fills rows 8 (wid + NW i) .. +7 of a slab
+  const uint8_t* __restrict__ X = reinterpret_cast<const uint8_t*>(a.x);
+  const int x_bytes = a.M * a.in_cs;
+  const int lrow = lane >> 3, pch = lane & 7;
+  int rrow[A_PW], roff[A_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    rrow[i] = 8 * (wid + NW * i) + lrow;
+    roff[i] = rrow[i] * a.in_cs + a.in_coff + ((pch ^ swz<64>(rrow[i])) << 4);
+  }
+  const int nst = (t1 - t0) * KC;
+  auto issue = [&](int s) {
+    const int tl = s / KC, ks = s - tl * KC;
+    const int px0 = (t0 + tl) * PT;
+    char* base = smem + (s % NS) * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) {
+      const int off = px0 + rrow[i] < a.M ? px0 * a.in_cs + roff[i] + ks * 128 : 0x7FFFFFF0;
+      buf_lds16(X, x_bytes, off, 0, base + (wid + NW * i) * 1024);
+    }
+  };
+  for (int s = 0; s < NS - 1 && s < nst; ++s) issue(s);
+
+  const bool exact = a.Cout == a.Cout_pad;  // then every full tile stores exactly NSTO times per wave
+  uint8_t* __restrict__ Y = reinterpret_cast<uint8_t*>(a.y) + a.out_coff;
+  const float osc = a.out_scale;
+  int t = 0;
+  for (int tl = 0; tl < t1 - t0; ++tl) {
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KC; ++ks, ++t) {
+      // wait for stage t: younger than its loads are the NS-2 later stages and
+      // the store batches of the tiles that ended in steps t-NS+1 .. t-1
+      if (t + NS - 2 >= nst) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      } else {
+        const int lo = t - NS + 1 > 0 ? t - NS + 1 : 0;  // tile ends: steps i KC + KC - 1
+        const int nb = exact && t >= KC ? (t - 1 - (KC - 1)) / KC - (lo + KC - 1 - (KC - 1)) / KC + 1 : 0;
+        wait_vm_counted<VM_RING, 0, (NS + KC - 2) / KC * NSTO>(nb * NSTO);
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + NS - 1 < nst) issue(t + NS - 1);
+      const char* B = smem + (t % NS) * STAGE;
+      i32x8 bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wp * TPW + j * 16 + (lane & 15);
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(B + row * 128 + ((c0 ^ swz<64>(row)) << 4));
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(B + row * 128 + (((c0 + 1) ^ swz<64>(row)) << 4));
+        bfr[j] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[ks][i], bfr[j], acc[i][j], 0, 0, 0, 127,
+                                                                       0, 127);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // epilogue from registers: no global loads here (one would make the compiler drain vmcnt)
+    const int pb = (t0 + tl) * PT + wp * TPW + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int co = cob + 16 * i + 4 * (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          v[q] = ycx_act<true>(fmaf(acc[i][j][q], qv[i][q], bv[i][q]), a.act, a.slope) * osc;
+        const uint32_t ov = f8x4_pack(v[0], v[1], v[2], v[3]);
+        const int p = pb + 16 * j;
+        if (p < a.M && co < a.Cout) *reinterpret_cast<uint32_t*>(Y + (size_t)p * a.out_cs + co) = ov;
+      }
+    }
+  }
+}
+
 ConvArgs make_args(const ycx_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                    const void* res) {
   ConvArgs a;
@@ -1947,6 +2080,7 @@ const TileInfo kTiles[] = {
     {64, 128, 64, "glds4w_co64_px128_k64_s2"},
     {128, 128, 16, "f8_co128_px128_k128_s2"},
     {64, 128, 16, "f8_co64_px128_k128_s2"},
+    {32, 64, 128, "f8_wres1x1"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -2065,6 +2199,37 @@ ycx_status launch_wres(ConvArgs a, hipStream_t st) {
   return launch_wres_k<2, 4, 32, 6, 1>(a, st);
 }
 
+bool wres_f8_ok(const ConvArgs& a) {
+  return a.KH == 1 && a.KW == 1 && a.S == 1 && a.P == 0 && a.H == a.Ho && a.W == a.Wo && !a.res &&
+         a.out_layout == YCX_OUT_NHWC && (a.Cin == 128 || a.Cin == 256 || a.Cin == 512) && a.Ktot == a.Cin &&
+         (a.Cout_pad == 64 || a.Cout_pad == 128 || a.Cout_pad % 256 == 0) &&
+         (long long)a.M * a.in_cs < (1LL << 31) - 64;
+}
+
+template <int WCO, int WPX, int TPW, int NS>
+ycx_status launch_wres_f8_k(ConvArgs a, hipStream_t st) {
+  a.n_ct = a.Cout_pad / (WCO * 32);
+  const int T = (a.M + TPW * WPX - 1) / (TPW * WPX);
+  const int R = std::max(1, std::min(T, 256 / a.n_ct));
+  a.nwg = R * a.n_ct;
+  dim3 g(a.nwg), b(WCO * WPX * 64);
+  switch (a.Cin) {
+    case 128: hipLaunchKernelGGL((conv1x1_wres_f8<WCO, WPX, TPW, 1, NS>), g, b, 0, st, a); break;
+    case 256: hipLaunchKernelGGL((conv1x1_wres_f8<WCO, WPX, TPW, 2, NS>), g, b, 0, st, a); break;
+    case 512: hipLaunchKernelGGL((conv1x1_wres_f8<WCO, WPX, TPW, 4, NS>), g, b, 0, st, a); break;
+    default: return YCX_ERR_UNSUPPORTED;
+  }
+  return ycx_launch_status();
+}
+
+// tile 36: the fp8 weight-resident 1x1 (persistent, one block per CU and channel group)
+ycx_status launch_wres_f8(ConvArgs a, hipStream_t st) {
+  if (!wres_f8_ok(a)) return YCX_ERR_UNSUPPORTED;
+  if (a.Cout_pad % 256 == 0) return launch_wres_f8_k<8, 1, 64, 5>(a, st);
+  if (a.Cout_pad == 128) return launch_wres_f8_k<4, 2, 64, 6>(a, st);
+  return launch_wres_f8_k<2, 4, 32, 6>(a, st);
+}
+
 }  // namespace
 
 extern "C" const char* ycx_conv_tile_name(int32_t tile) {
@@ -2077,8 +2242,17 @@ extern "C" const char* ycx_conv_tile_name(int32_t tile) {
 static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wres: no residual (tiles 22, 23)
   if (d->dtype == YCX_DT_F32) return 8;
   const long long M = (long long)d->n * d->ho * d->wo;
-  if (d->dtype == YCX_DT_FP8)
+  if (d->dtype == YCX_DT_FP8) {
+    // pointwise layers with cin in {128, 256, 512} and >= 8 pixel tiles per persistent block:
+    // weights resident in registers (tile 36)
+    if (allow_wres && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && d->out_layout == YCX_OUT_NHWC &&
+        (d->cin == 128 || d->cin == 256 || d->cin == 512) &&
+        (d->cout_pad == 64 || d->cout_pad == 128 || d->cout_pad % 256 == 0)) {
+      const long long pt = d->cout_pad >= 256 ? 64 : 128, groups = d->cout_pad >= 256 ? d->cout_pad / 256 : 1;
+      if (M >= 8 * pt * (256 / groups)) return 36;
+    }
     return d->cout_pad % 128 == 0 && (d->cout_pad / 128) * ((M + 127) / 128) >= 256 ? 34 : 35;
+  }
   const bool k64 = (d->cin % 64) == 0;
   if (d->cout_pad % 64 != 0) return 5;  // cout 32: co32 x px256, BK 32 (cin % 32 == 0)
   // The 512-thread LDS-DMA kernels' buffer descriptors address < 2 GiB per operand.
@@ -2160,10 +2334,11 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
   YCX_CHECK_SUPPORTED(tile > 0 && tile < kNumTiles);
   const TileInfo& t = kTiles[tile];
   YCX_CHECK_SUPPORTED(d->cin % t.bk == 0 && d->cout_pad % t.bm == 0);
-  YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_FP8) == (tile == 34 || tile == 35));
+  YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_FP8) == (tile == 34 || tile == 35 || tile == 36));
   if (d->dtype == YCX_DT_FP8) {
     YCX_CHECK_SUPPORTED((long long)d->cout_pad * a.Ktot < (1LL << 31) &&
                         (long long)d->n * d->h * d->w * d->in_c_stride < (1LL << 31) - 64);
+    if (tile == 36) return launch_wres_f8(a, st);
     return tile == 34 ? launch_f8<128, 128, 2, 4>(a, st) : launch_f8<64, 128, 1, 8>(a, st);
   }
   if (d->dtype == YCX_DT_F32) {

@@ -167,6 +167,25 @@ def check(status: int, what: str = "") -> None:
         raise YcxError(status, what)
 
 
+def dedicated_stream(device, priority: int = 0):
+    """A non-blocking HIP stream of our own (hipStreamCreateWithPriority), wrapped
+    as a torch ExternalStream: unlike torch.cuda.Stream() it is not one of the
+    pool streams that every other component (the RCCL communicator included)
+    is handed round-robin, so no other work can share it. Never destroyed."""
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already loaded (same soname)
+    s = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = hip.hipStreamCreateWithPriority(ctypes.byref(s), ctypes.c_uint(1), ctypes.c_int(priority))
+    if rc != 0:
+        raise RuntimeError(f"ycx: hipStreamCreateWithPriority failed ({rc})")
+    _STREAMS.append(s.value)
+    return torch.cuda.ExternalStream(s.value, device=device)
+
+
+_STREAMS = []
+
+
 def ptr(t) -> int | None:
     """Device pointer of a tensor (None passes a null pointer)."""
     return None if t is None else t.data_ptr()
