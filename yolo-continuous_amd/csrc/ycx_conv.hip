@@ -547,6 +547,14 @@ __device__ __forceinline__ uint32_t f8x4_pack(float a, float b, float c, float d
   return (uint32_t)w;
 }
 
+// Row swizzle of the fp8 128-B LDS rows. An fp8 fragment read takes two
+// consecutive 16-B chunks per lane (2g, 2g + 1 of its row, g = lane >> 4), and
+// with this swizzle every ds_read_b128 lane group hits 16 distinct bank
+// granules for any 16-row-aligned fragment (brute-forced over the four lane
+// groups and both reads; the bf16 kernels' swz<64> is 2-way there). The DMA
+// slab rows 8 (w + NW i) + lrow give swz8 = f(lrow, w & 1): one logical chunk per lane.
+__device__ __forceinline__ int swz8(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 2); }
+
 // 4 consecutive fp8 output channels of pixel p (residual added first, then scaled).
 __device__ __forceinline__ void store4_f8(const ConvArgs& a, int p, int co, float v[4]) {
   if (a.res) {
@@ -642,11 +650,11 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a) {
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     const int row = 8 * (wid + NW * i) + lrow;
-    a_off[i] = (co0 + row) * a.Ktot + ((pch ^ swz<64>(row)) << 4);
+    a_off[i] = (co0 + row) * a.Ktot + ((pch ^ swz8(row)) << 4);
   }
-  // swz<64>(row) = (4 (wid + NW i) + lrow / 2) & 7 = (4 wid + lrow / 2) & 7 for every i:
-  // the logical chunk (so the tap select) of a lane is the same in all its slabs.
-  const int lch = pch ^ swz<64>(8 * wid + lrow);
+  // swz8(8 (wid + NW i) + lrow) depends on lrow and wid & 1 only (NW even): the logical
+  // chunk (so the tap select) of a lane is the same in all its slabs.
+  const int lch = pch ^ swz8(8 * wid + lrow);
   // TPS 0: lane chunk k = 128 s + 16 lch -> (tap, channel) = divmod(k, cin), tracked per lane
   const int tsel = TPS == 1 ? 0 : TPS == 0 ? (16 * lch) / a.Cin : lch / CPT;
   const int cbyte = TPS == 0 ? 0 : (TPS == 1 ? lch : lch % CPT) << 4;
@@ -720,15 +728,15 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int row = wm * TM + i * 16 + (lane & 15);
-      const i32x4 lo = *reinterpret_cast<const i32x4*>(A + row * RB + ((c0 ^ swz<64>(row)) << 4));
-      const i32x4 hi = *reinterpret_cast<const i32x4*>(A + row * RB + (((c0 + 1) ^ swz<64>(row)) << 4));
+      const i32x4 lo = *reinterpret_cast<const i32x4*>(A + row * RB + ((c0 ^ swz8(row)) << 4));
+      const i32x4 hi = *reinterpret_cast<const i32x4*>(A + row * RB + (((c0 + 1) ^ swz8(row)) << 4));
       af[i] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int row = wn * TN + j * 16 + (lane & 15);
-      const i32x4 lo = *reinterpret_cast<const i32x4*>(B + row * RB + ((c0 ^ swz<64>(row)) << 4));
-      const i32x4 hi = *reinterpret_cast<const i32x4*>(B + row * RB + (((c0 + 1) ^ swz<64>(row)) << 4));
+      const i32x4 lo = *reinterpret_cast<const i32x4*>(B + row * RB + ((c0 ^ swz8(row)) << 4));
+      const i32x4 hi = *reinterpret_cast<const i32x4*>(B + row * RB + (((c0 + 1) ^ swz8(row)) << 4));
       bfr[j] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -1946,7 +1954,7 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     rrow[i] = 8 * (wid + NW * i) + lrow;
-    roff[i] = rrow[i] * a.in_cs + a.in_coff + ((pch ^ swz<64>(rrow[i])) << 4);
+    roff[i] = rrow[i] * a.in_cs + a.in_coff + ((pch ^ swz8(rrow[i])) << 4);
   }
   const int nst = (t1 - t0) * KC;
   auto issue = [&](int s) {
@@ -1990,8 +1998,8 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int row = wp * TPW + j * 16 + (lane & 15);
-        const i32x4 lo = *reinterpret_cast<const i32x4*>(B + row * 128 + ((c0 ^ swz<64>(row)) << 4));
-        const i32x4 hi = *reinterpret_cast<const i32x4*>(B + row * 128 + (((c0 + 1) ^ swz<64>(row)) << 4));
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(B + row * 128 + ((c0 ^ swz8(row)) << 4));
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(B + row * 128 + (((c0 + 1) ^ swz8(row)) << 4));
         bfr[j] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
@@ -2016,6 +2024,138 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
         const uint32_t ov = f8x4_pack(v[0], v[1], v[2], v[3]);
         const int p = pb + 16 * j;
         if (p < a.M && co < a.Cout) *reinterpret_cast<uint32_t*>(Y + (size_t)p * a.out_cs + co) = ov;
+      }
+    }
+  }
+}
+
+// -------------------------------------------------------------------------
+// fp8 weight-stationary 3x3 64 -> 64 (tile 37): conv3x3_ws64 on the e4m3
+// block-scaled MFMA. One K step of 128 = two taps x 64 channels, so the nine
+// taps are five steps (the tenth tap's weights are the zero padding of the
+// 640-byte weight rows, its B operand any finite pixel). Persistent 512-thread
+// block per CU: all five 128-byte weight slices of the 64 output channels in
+// LDS (40 KB, chunk q of row (step, co) at q ^ swz(co)); 16x16 output tiles
+// whose 18x18 halo (64 B per pixel) is LDS-DMA'd into the second buffer while
+// the current tile computes. Halo chunk q of pixel h lives at q ^ ((h >> 2) & 1):
+// with the 16x16x128 B-fragment lane map (lane -> pixel l & 15, chunk pair of
+// group l >> 4) every ds_read_b128 lane group then hits 16 distinct 16-B bank
+// granules at any halo offset (brute-forced over all offsets). Epilogue:
+// act(acc * dq + bias) * out_scale -> e4m3, 4 B per lane; the stores enter the
+// next tile's counted vmcnt wait.
+// -------------------------------------------------------------------------
+template <int ACT>
+__global__ void __launch_bounds__(512) conv3x3_ws64_f8(ConvArgs a) {
+  constexpr int NW = 8, TH = 16, TW = 16, HW = TW + 2, HP = (TH + 2) * HW;  // 324 halo pixels
+  constexpr int HPIECES = (HP + 15) / 16, HPW = (HPIECES + NW - 1) / NW;    // 1-KB DMA pieces (16 pixels)
+  constexpr int HBUF = HPIECES * 1024, WBYTES = 5 * 64 * 128;
+  constexpr int FM = 2, FN = 4;
+  __shared__ __attribute__((aligned(1024))) char smem[WBYTES + 2 * HBUF];
+  char* const wl = smem;
+  const uint8_t* __restrict__ X = reinterpret_cast<const uint8_t*>(a.x);
+  const uint8_t* __restrict__ Wt = reinterpret_cast<const uint8_t*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int tx_n = a.Wo / TW, tpi = (a.Ho / TH) * tx_n, ntiles = a.N * tpi;
+  const int blk = ycx_xcd_remap(blockIdx.x, gridDim.x);
+  const int tb = (int)((long long)blk * ntiles / gridDim.x), te = (int)((long long)(blk + 1) * ntiles / gridDim.x);
+  if (tb >= te) return;
+  const int w_bytes = a.Cout_pad * a.Ktot, x_bytes = a.N * a.H * a.W * a.in_cs;
+
+  // weights: LDS row R = 64 step + co (128 B), logical chunk q at q ^ swz(co); 40 pieces, 5 per wave
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int R = 8 * (wid + NW * i) + lrow, st = R >> 6, co = R & 63;
+    buf_lds16(Wt, w_bytes, co * a.Ktot + st * 128 + ((pch ^ swz8(co)) << 4), 0, wl + (wid + NW * i) * 1024);
+  }
+  // halo of a tile into buffer b: a 1-KB piece is 16 pixels; lane -> pixel (lane >> 2), physical chunk lane & 3
+  auto issue_h = [&](int tile, int b) {
+    const int n = tile / tpi, ti = tile - n * tpi;
+    const int oy0 = (ti / tx_n) * TH, ox0 = (ti % tx_n) * TW;
+#pragma unroll
+    for (int i = 0; i < HPW; ++i) {
+      const int piece = wid + NW * i;
+      if (piece >= HPIECES) break;  // uniform
+      const int h = 16 * piece + (lane >> 2), hy = h / HW, hx = h - hy * HW;
+      const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
+      const bool ok = h < HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      const int lc = (lane & 3) ^ ((h >> 2) & 1);  // logical chunk this lane fetches
+      buf_lds16(X, x_bytes, ok ? ((n * a.H + iy) * a.W + ix) * a.in_cs + a.in_coff + (lc << 4) : 0x7FFFFFF0, 0,
+                smem + WBYTES + b * HBUF + piece * 1024);
+    }
+  };
+  issue_h(tb, 0);
+  f32x4 bv[FM], qv[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int co = 32 * wm + 16 * i + 4 * (lane >> 4);
+    const bool ok = co < a.Cout;
+    bv[i] = ok ? *reinterpret_cast<const f32x4*>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+    qv[i] = ok ? *reinterpret_cast<const f32x4*>(a.bias + a.Cout_pad + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bool exact = a.Cout == 64;  // then every tile stores FM x FN times per wave
+  uint8_t* __restrict__ Y = reinterpret_cast<uint8_t*>(a.y) + a.out_coff;
+  const float osc = a.out_scale;
+  const int g = lane >> 4, c0 = 2 * g;   // A: chunk pair of the 128-B row
+  const int hc2 = 2 * (g & 1);            // B: channel half (chunk pair) of the tap
+
+  for (int tile = tb; tile < te; ++tile) {
+    const int b = (tile - tb) & 1;
+    if (tile > tb && exact) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FM * FN) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // this tile's halo (and the weights) landed; the other buffer is free
+    if (tile + 1 < te) issue_h(tile + 1, b ^ 1);
+    const char* halo = smem + WBYTES + b * HBUF;
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int st = 0; st < 5; ++st) {  // not unrolled: hoisting 5 steps' lane addresses spills
+      int t = 2 * st + (g >> 1);
+      t = t > 8 ? 8 : t;  // the tenth tap: zero weights, any finite pixel
+      const int ky = t / 3, kx = t - 3 * ky;
+      i32x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int co = 32 * wm + 16 * i + (lane & 15);
+        const char* row = wl + (st * 64 + co) * 128;
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(row + ((c0 ^ swz8(co)) << 4));
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(row + (((c0 + 1) ^ swz8(co)) << 4));
+        af[i] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int h = (wn * FN + j + ky) * HW + (lane & 15) + kx;
+        const int sw = (h >> 2) & 1;
+        const char* px = halo + h * 64;
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(px + ((hc2 ^ sw) << 4));
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(px + (((hc2 + 1) ^ sw) << 4));
+        bfr[j] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+      __builtin_amdgcn_sched_barrier(0);  // one step's fragments live at a time
+    }
+    // epilogue: e4m3 4-byte stores from registers (no global loads: they would drain vmcnt)
+    const int n = tile / tpi, ti = tile - n * tpi;
+    const int oy0 = (ti / tx_n) * TH, ox0 = (ti % tx_n) * TW;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int co = 32 * wm + 16 * i + 4 * (lane >> 4);
+      if (co >= a.Cout) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int p = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0 + (lane & 15);
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = act_t<ACT>(fmaf(acc[i][j][q], qv[i][q], bv[i][q]), a.slope) * osc;
+        *reinterpret_cast<uint32_t*>(Y + (size_t)p * a.out_cs + co) = f8x4_pack(v[0], v[1], v[2], v[3]);
       }
     }
   }
@@ -2081,6 +2221,7 @@ const TileInfo kTiles[] = {
     {128, 128, 16, "f8_co128_px128_k128_s2"},
     {64, 128, 16, "f8_co64_px128_k128_s2"},
     {32, 64, 128, "f8_wres1x1"},
+    {64, 256, 64, "f8_halo3x3_ws_co64"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -2222,6 +2363,22 @@ ycx_status launch_wres_f8_k(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
+// tile 37: fp8 weight-stationary 3x3 64 -> 64, one persistent block per CU
+ycx_status launch_ws64_f8(ConvArgs a, hipStream_t st) {
+  if (!(a.KH == 3 && a.KW == 3 && a.S == 1 && a.P == 1 && a.H == a.Ho && a.W == a.Wo && a.Ho % 16 == 0 &&
+        a.Wo % 16 == 0 && a.Cin == 64 && a.Cout_pad == 64 && a.Ktot == 640 && a.out_layout == YCX_OUT_NHWC &&
+        !a.res && (long long)a.N * a.H * a.W * a.in_cs < (1LL << 31) - 64))
+    return YCX_ERR_UNSUPPORTED;
+  const long long ntiles = (long long)a.N * (a.Ho / 16) * (a.Wo / 16);
+  const dim3 g((unsigned)std::min<long long>(ntiles, 256)), b(512);
+  switch (a.act) {
+    case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3_ws64_f8<YCX_ACT_SILU>), g, b, 0, st, a); break;
+    case YCX_ACT_LEAKY: hipLaunchKernelGGL((conv3x3_ws64_f8<YCX_ACT_LEAKY>), g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3x3_ws64_f8<YCX_ACT_NONE>), g, b, 0, st, a); break;
+  }
+  return ycx_launch_status();
+}
+
 // tile 36: the fp8 weight-resident 1x1 (persistent, one block per CU and channel group)
 ycx_status launch_wres_f8(ConvArgs a, hipStream_t st) {
   if (!wres_f8_ok(a)) return YCX_ERR_UNSUPPORTED;
@@ -2251,6 +2408,11 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
       const long long pt = d->cout_pad >= 256 ? 64 : 128, groups = d->cout_pad >= 256 ? d->cout_pad / 256 : 1;
       if (M >= 8 * pt * (256 / groups)) return 36;
     }
+    // 3x3 / s1 64 -> 64 'same' convs on 16-aligned maps with >= 2 tiles per block: weights in LDS (tile 37)
+    if (allow_wres && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->h == d->ho &&
+        d->w == d->wo && d->ho % 16 == 0 && d->wo % 16 == 0 && d->cin == 64 && d->cout_pad == 64 &&
+        d->out_layout == YCX_OUT_NHWC && (long long)d->n * (d->ho / 16) * (d->wo / 16) >= 512)
+      return 37;
     return d->cout_pad % 128 == 0 && (d->cout_pad / 128) * ((M + 127) / 128) >= 256 ? 34 : 35;
   }
   const bool k64 = (d->cin % 64) == 0;
@@ -2334,11 +2496,12 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
   YCX_CHECK_SUPPORTED(tile > 0 && tile < kNumTiles);
   const TileInfo& t = kTiles[tile];
   YCX_CHECK_SUPPORTED(d->cin % t.bk == 0 && d->cout_pad % t.bm == 0);
-  YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_FP8) == (tile == 34 || tile == 35 || tile == 36));
+  YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_FP8) == (tile >= 34 && tile <= 37));
   if (d->dtype == YCX_DT_FP8) {
     YCX_CHECK_SUPPORTED((long long)d->cout_pad * a.Ktot < (1LL << 31) &&
                         (long long)d->n * d->h * d->w * d->in_c_stride < (1LL << 31) - 64);
     if (tile == 36) return launch_wres_f8(a, st);
+    if (tile == 37) return launch_ws64_f8(a, st);
     return tile == 34 ? launch_f8<128, 128, 2, 4>(a, st) : launch_f8<64, 128, 1, 8>(a, st);
   }
   if (d->dtype == YCX_DT_F32) {
