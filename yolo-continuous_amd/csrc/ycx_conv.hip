@@ -2382,9 +2382,15 @@ ycx_status launch_ws64_f8(ConvArgs a, hipStream_t st) {
 // tile 36: the fp8 weight-resident 1x1 (persistent, one block per CU and channel group)
 ycx_status launch_wres_f8(ConvArgs a, hipStream_t st) {
   if (!wres_f8_ok(a)) return YCX_ERR_UNSUPPORTED;
-  if (a.Cout_pad % 256 == 0) return launch_wres_f8_k<8, 1, 64, 5>(a, st);
-  if (a.Cout_pad == 128) return launch_wres_f8_k<4, 2, 64, 6>(a, st);
-  return launch_wres_f8_k<2, 4, 32, 6>(a, st);
+#ifndef YCX_F8W_NS
+#define YCX_F8W_NS 5
+#endif
+#ifndef YCX_F8W_NS2
+#define YCX_F8W_NS2 6
+#endif
+  if (a.Cout_pad % 256 == 0) return launch_wres_f8_k<8, 1, 64, YCX_F8W_NS>(a, st);
+  if (a.Cout_pad == 128) return launch_wres_f8_k<4, 2, 64, YCX_F8W_NS2>(a, st);
+  return launch_wres_f8_k<2, 4, 32, YCX_F8W_NS2>(a, st);
 }
 
 }  // namespace
