@@ -1911,7 +1911,7 @@ template <int WCO, int WPX, int TPW, int KC, int NS>
 __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
   constexpr int NW = WCO * WPX, PT = TPW * WPX, FM = 2, FN = TPW / 16, BCO = WCO * 32;
   constexpr int STAGE = PT * 128, A_PW = PT / (8 * NW);
-  constexpr int NSTO = FM * FN;  // dword stores per wave per tile
+  constexpr int NSTO = FN;  // 8-byte stores per wave per tile (A rows permuted: 8 channels per lane)
   constexpr int VM_RING = A_PW * (NS - 2);
   static_assert(A_PW >= 1 && PT % (8 * NW) == 0 && TPW % 16 == 0, "tile rows per wave");
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
@@ -1926,21 +1926,24 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
   const int cob = g * BCO + wc * 32;
   const int c0 = 2 * (lane >> 4);
 
-  // this wave's weights: A fragment (slab s, i) = bytes 128 s + 16 c0 .. +31 of row cob + 16 i + (lane & 15)
+  // this wave's weights: A fragment (slab s, i) = bytes 128 s + 16 c0 .. +31 of the weight row of
+  // channel cob + 8 (m >> 2) + 4 i + (m & 3), m = lane & 15: the C rows 4g .. 4g+3 of fragments 0
+  // and 1 are then channels 8g .. 8g+7 of the wave's 32, one 8-byte e4m3 store per lane and pixel
   const uint8_t* __restrict__ Wt = reinterpret_cast<const uint8_t*>(a.w);
   i32x8 af[KC][FM];
 #pragma unroll
   for (int s = 0; s < KC; ++s)
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const uint8_t* w = Wt + (size_t)(cob + 16 * i + (lane & 15)) * a.Ktot + 128 * s + 16 * c0;
+      const int m = lane & 15;
+      const uint8_t* w = Wt + (size_t)(cob + 8 * (m >> 2) + 4 * i + (m & 3)) * a.Ktot + 128 * s + 16 * c0;
       const i32x4 lo = *reinterpret_cast<const i32x4*>(w), hi = *reinterpret_cast<const i32x4*>(w + 16);
       af[s][i] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
   f32x4 bv[FM], qv[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int co = cob + 16 * i + 4 * (lane >> 4);
+    const int co = cob + 8 * (lane >> 4) + 4 * i;
     const bool ok = co < a.Cout;
     bv[i] = ok ? *reinterpret_cast<const f32x4*>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
     qv[i] = ok ? *reinterpret_cast<const f32x4*>(a.bias + a.Cout_pad + co) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -2012,19 +2015,18 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
     }
     // epilogue from registers: no global loads here (one would make the compiler drain vmcnt)
     const int pb = (t0 + tl) * PT + wp * TPW + (lane & 15);
+    const int co = cob + 8 * (lane >> 4);  // channels co .. co+7 (cout % 8 == 0: all valid or none)
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int co = cob + 16 * i + 4 * (lane >> 4);
+    for (int j = 0; j < FN; ++j) {
+      float v[8];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        float v[4];
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          v[q] = ycx_act<true>(fmaf(acc[i][j][q], qv[i][q], bv[i][q]), a.act, a.slope) * osc;
-        const uint32_t ov = f8x4_pack(v[0], v[1], v[2], v[3]);
-        const int p = pb + 16 * j;
-        if (p < a.M && co < a.Cout) *reinterpret_cast<uint32_t*>(Y + (size_t)p * a.out_cs + co) = ov;
-      }
+          v[4 * i + q] = ycx_act<true>(fmaf(acc[i][j][q], qv[i][q], bv[i][q]), a.act, a.slope) * osc;
+      const uint2 ov = make_uint2(f8x4_pack(v[0], v[1], v[2], v[3]), f8x4_pack(v[4], v[5], v[6], v[7]));
+      const int p = pb + 16 * j;
+      if (p < a.M && co < a.Cout) *reinterpret_cast<uint2*>(Y + (size_t)p * a.out_cs + co) = ov;
     }
   }
 }
@@ -2388,7 +2390,10 @@ ycx_status launch_wres_f8(ConvArgs a, hipStream_t st) {
 #ifndef YCX_F8W_NS2
 #define YCX_F8W_NS2 6
 #endif
-  if (a.Cout_pad % 256 == 0) return launch_wres_f8_k<8, 1, 64, YCX_F8W_NS>(a, st);
+#ifndef YCX_F8W_TPW
+#define YCX_F8W_TPW 64
+#endif
+  if (a.Cout_pad % 256 == 0) return launch_wres_f8_k<8, 1, YCX_F8W_TPW, YCX_F8W_NS>(a, st);
   if (a.Cout_pad == 128) return launch_wres_f8_k<4, 2, 64, YCX_F8W_NS2>(a, st);
   return launch_wres_f8_k<2, 4, 32, YCX_F8W_NS2>(a, st);
 }
