@@ -1781,7 +1781,7 @@ template <int WCO, int WPX, int TPW, int KC, int NS, int SUB>
 __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
   constexpr int NW = WCO * WPX, PT = TPW * WPX, FM = 2, FN = TPW / 16, BCO = WCO * 32;
   constexpr int KS = KC / SUB, SLAB = PT * 128, STAGE = SUB * SLAB, A_PW = PT / (8 * NW);
-  constexpr int NSTO = FM * FN;  // bf16x4 stores per wave per tile
+  constexpr int NSTO = FN;  // 16-byte stores per wave per tile (A rows permuted: 8 channels per lane)
   constexpr int VM_RING = A_PW * SUB * (NS - 2);
   static_assert(KC % SUB == 0, "slabs per stage");
   static_assert(A_PW >= 1 && PT % (8 * NW) == 0 && TPW % 16 == 0, "tile rows per wave");
@@ -1796,19 +1796,22 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
   if (t0 >= t1) return;  // whole block: no barrier is left waiting
   const int cob = g * BCO + wc * 32;
 
-  // this wave's weights (A fragments: co = cob + 16 i + (lane & 15), k = 32 kq + 8 (lane >> 4) ..)
+  // this wave's weights (A fragments: row m = lane & 15 of fragment i is channel
+  // cob + 8 (m >> 2) + 4 i + (m & 3), k = 32 kq + 8 (lane >> 4) ..): the C rows 4g .. 4g+3 of
+  // fragments 0 and 1 are then channels 8g .. 8g+7, one 16-byte store per lane and pixel
   const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
   bf16x8 af[2 * KC][FM];
+  const int m16 = lane & 15;
 #pragma unroll
   for (int kq = 0; kq < 2 * KC; ++kq)
 #pragma unroll
     for (int i = 0; i < FM; ++i)
-      af[kq][i] = *reinterpret_cast<const bf16x8*>(Wt + (size_t)(cob + 16 * i + (lane & 15)) * a.Ktot + 32 * kq +
-                                                   8 * (lane >> 4));
+      af[kq][i] = *reinterpret_cast<const bf16x8*>(Wt + (size_t)(cob + 8 * (m16 >> 2) + 4 * i + (m16 & 3)) * a.Ktot +
+                                                   32 * kq + 8 * (lane >> 4));
   f32x4 bv[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int co = cob + 16 * i + 4 * (lane >> 4);
+    const int co = cob + 8 * (lane >> 4) + 4 * i;
     bv[i] = co < a.Cout ? *reinterpret_cast<const f32x4*>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
@@ -1881,17 +1884,16 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
     }
     // epilogue from registers: no global loads here (one would make the compiler drain vmcnt)
     const int pb = (t0 + tl) * PT + wp * TPW + (lane & 15);
+    const int co = cob + 8 * (lane >> 4);  // channels co .. co+7 (cout % 8 == 0: all valid or none)
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int co = cob + 16 * i + 4 * (lane >> 4);
+    for (int j = 0; j < FN; ++j) {
+      bf16x8 ov;
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        bf16x4 ov;
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ov[q] = (__bf16)ycx_act<true>(acc[i][j][q] + bv[i][q], a.act, a.slope);
-        const int p = pb + 16 * j;
-        if (p < a.M && co < a.Cout) *reinterpret_cast<bf16x4*>(Y + (size_t)p * a.out_cs + co) = ov;
-      }
+        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (__bf16)ycx_act<true>(acc[i][j][q] + bv[i][q], a.act, a.slope);
+      const int p = pb + 16 * j;
+      if (p < a.M && co < a.Cout) *reinterpret_cast<bf16x8*>(Y + (size_t)p * a.out_cs + co) = ov;
     }
   }
 }
