@@ -339,6 +339,33 @@ __device__ __forceinline__ void epilogue_regs(const ConvArgs& a, const f32x4 (&a
   }
 }
 
+// NHWC epilogue for permuted A rows (conv_bf16_glds): fragments 2k, 2k+1 hold channels
+// cob + 32k + 8g .. +7 in C rows 4g..4g+3 (g = lane >> 4): one 16-byte store per lane and pixel
+// (store8: residual and x2 upsample included).
+template <int FM, int FN>
+__device__ __forceinline__ void epilogue_regs8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob, int pxb,
+                                               int lane) {
+#pragma unroll
+  for (int k = 0; k < FM / 2; ++k) {
+    const int co = cob + 32 * k + 8 * (lane >> 4);
+    if (co >= a.Cout) continue;  // cout % 8 == 0: the 8 channels are all valid
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + co);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bias + co + 4);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int p = pxb + j * 16 + (lane & 15);
+      if (p >= a.M) continue;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = ycx_act<true>(acc[2 * k][j][r] + b0[r], a.act, a.slope);
+        v[4 + r] = ycx_act<true>(acc[2 * k + 1][j][r] + b1[r], a.act, a.slope);
+      }
+      store8<__bf16>(a, p, co, v);
+    }
+  }
+}
+
 // Same, for fragments whose 16 pixels start at arbitrary pixel indices pxf[j].
 template <int FM, int FN>
 __device__ __forceinline__ void epilogue_frag(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob,
@@ -411,11 +438,17 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
   // num_records makes the LDS-DMA write zeros (measured on gfx950) — the
   // padding taps and the pixel tail cost no branch and no zero page.
   const int w_bytes = a.Cout_pad * a.Ktot * 2, x_bytes = a.N * a.H * a.W * a.in_cs * 2;
+  // NHWC outputs with an even fragment count: LDS row wm TM + 16 f + m holds channel
+  // wm TM + 32 (f >> 1) + 8 (m >> 2) + 4 (f & 1) + (m & 3), so C rows 4g..4g+3 of fragments 2k and
+  // 2k+1 are 8 consecutive channels and the epilogue stores 16 bytes per lane and pixel
+  const bool perm = (FM % 2 == 0) && a.out_layout != YCX_OUT_NCHW_F32;
   int a_off[A_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     const int row = 8 * (wid + NW * i) + lrow;
-    a_off[i] = ((co0 + row) * a.Ktot + ((pch ^ swz<BK>(row)) << 3)) * 2;
+    const int f = (row % TM) >> 4, m = row & 15;
+    const int ch = perm ? (row / TM) * TM + 32 * (f >> 1) + 8 * (m >> 2) + 4 * (f & 1) + (m & 3) : row;
+    a_off[i] = ((co0 + ch) * a.Ktot + ((pch ^ swz<BK>(row)) << 3)) * 2;
   }
   int b_iy0[B_PW], b_ix0[B_PW], b_base[B_PW];
 #pragma unroll
@@ -513,6 +546,12 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (FM % 2 == 0) {
+    if (perm) {
+      epilogue_regs8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+      return;
+    }
   }
   epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
 }
