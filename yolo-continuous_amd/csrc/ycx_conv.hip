@@ -339,6 +339,29 @@ __device__ __forceinline__ void epilogue_regs(const ConvArgs& a, const f32x4 (&a
   }
 }
 
+// epilogue_regs8 for fragments whose 16 pixels start at arbitrary pixel indices pxf[j].
+template <int FM, int FN>
+__device__ __forceinline__ void epilogue_frag8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob,
+                                               const int (&pxf)[FN], int lane) {
+#pragma unroll
+  for (int k = 0; k < FM / 2; ++k) {
+    const int co = cob + 32 * k + 8 * (lane >> 4);
+    if (co >= a.Cout) continue;
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + co);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bias + co + 4);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = ycx_act<true>(acc[2 * k][j][r] + b0[r], a.act, a.slope);
+        v[4 + r] = ycx_act<true>(acc[2 * k + 1][j][r] + b1[r], a.act, a.slope);
+      }
+      store8<__bf16>(a, pxf[j] + (lane & 15), co, v);
+    }
+  }
+}
+
 // NHWC epilogue for permuted A rows (conv_bf16_glds): fragments 2k, 2k+1 hold channels
 // cob + 32k + 8g .. +7 in C rows 4g..4g+3 (g = lane >> 4): one 16-byte store per lane and pixel
 // (store8: residual and x2 upsample included).
@@ -1085,11 +1108,14 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
   if (tb >= te) return;
   const int w_bytes = a.Cout_pad * a.Ktot * 2, x_bytes = a.N * a.H * a.W * a.in_cs * 2;
 
-  // weights: LDS row R = 64 tap + co (128 B), logical chunk q at q ^ swz(co); 72 pieces, 9 per wave
+  // weights: LDS row R = 64 tap + co (128 B), logical chunk q at q ^ swz(co); 72 pieces, 9 per wave.
+  // LDS row co holds channel 32 (co >> 5) + 8 (m >> 2) + 4 f + (m & 3) (f = co >> 4 & 1, m = co & 15):
+  // C rows 4g..4g+3 of the two fragments are channels 32 wm + 8g .. +7, one 16-byte store per lane
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
-    const int R = 8 * (wid + NW * i) + lrow, t = R >> 6, co = R & 63;
-    buf_lds16(Wt, w_bytes, (co * a.Ktot + t * 64 + ((pch ^ swz<64>(co)) << 3)) * 2, 0, wl + (wid + NW * i) * 1024);
+    const int R = 8 * (wid + NW * i) + lrow, t = R >> 6, co = R & 63, m = co & 15;
+    const int ch = (co & 32) + 8 * (m >> 2) + 4 * ((co >> 4) & 1) + (m & 3);
+    buf_lds16(Wt, w_bytes, (ch * a.Ktot + t * 64 + ((pch ^ swz<64>(co)) << 3)) * 2, 0, wl + (wid + NW * i) * 1024);
   }
   // halo of a tile into buffer b: halo pixel h keeps its chunk q at q ^ (h & 7)
   auto issue_h = [&](int tile, int b) {
@@ -1110,15 +1136,15 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
   f32x4 bv[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int co = 32 * wm + 16 * i + 4 * (lane >> 4);
+    const int co = 32 * wm + 8 * (lane >> 4) + 4 * i;
     bv[i] = co < a.Cout ? *reinterpret_cast<const f32x4*>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const bool exact = a.Cout == 64;  // then every tile stores FM x FN times per wave
+  const bool exact = a.Cout == 64;  // then every tile stores FN times per wave
   __bf16* __restrict__ Y = reinterpret_cast<__bf16*>(a.y) + a.out_coff;
 
   for (int tile = tb; tile < te; ++tile) {
     const int b = (tile - tb) & 1;
-    if (tile > tb && exact) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FM * FN) : "memory");
+    if (tile > tb && exact) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FN) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // this tile's halo (and the weights) landed; the other buffer is free
     if (tile + 1 < te) issue_h(tile + 1, b ^ 1);
@@ -1152,20 +1178,20 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
-    // epilogue: act, 8-byte stores from registers (no global loads: they would drain vmcnt)
+    // epilogue: act, 16-byte stores from registers (no global loads: they would drain vmcnt)
     const int n = tile / tpi, ti = tile - n * tpi;
     const int oy0 = (ti / tx_n) * TH, ox0 = (ti % tx_n) * TW;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int co = 32 * wm + 16 * i + 4 * (lane >> 4);
-      if (co >= a.Cout) continue;
+    const int co = 32 * wm + 8 * (lane >> 4);
+    if (co < a.Cout) {  // cout % 8 == 0: the 8 channels are all valid
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int p = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0 + (lane & 15);
-        bf16x4 ov;
+        bf16x8 ov;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ov[q] = (__bf16)act_t<ACT>(acc[i][j][q], a.slope);
-        *reinterpret_cast<bf16x4*>(Y + (size_t)p * a.out_cs + co) = ov;
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ov[4 * i + q] = (__bf16)act_t<ACT>(acc[i][j][q], a.slope);
+        *reinterpret_cast<bf16x8*>(Y + (size_t)p * a.out_cs + co) = ov;
       }
     }
   }
@@ -1196,11 +1222,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3x3_halo(ConvArgs a) {
   const int lrow = lane >> 3, pch = lane & 7;
   const int w_bytes = a.Cout_pad * a.Ktot * 2, x_bytes = a.N * a.H * a.W * a.in_cs * 2;
 
+  // permuted A rows as in conv_bf16_glds: 16-byte epilogue stores
   int a_off[A_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     const int row = 8 * (wid + NW * i) + lrow;
-    a_off[i] = ((co0 + row) * a.Ktot + ((pch ^ swz<64>(row)) << 3)) * 2;
+    const int f = (row % TM) >> 4, m = row & 15;
+    const int ch = FM % 2 == 0 ? (row / TM) * TM + 32 * (f >> 1) + 8 * (m >> 2) + 4 * (f & 1) + (m & 3) : row;
+    a_off[i] = ((co0 + ch) * a.Ktot + ((pch ^ swz<64>(row)) << 3)) * 2;
   }
   int h_off[HPW];  // halo piece i of this wave: byte offset of the lane's chunk (chunk 0 of the tap), or -1
 #pragma unroll
@@ -1278,7 +1307,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3x3_halo(ConvArgs a) {
   int pxf[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) pxf[j] = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0;
-  epilogue_frag<FM, FN>(a, acc, co0 + wm * TM, pxf, lane);
+  if constexpr (FM % 2 == 0) epilogue_frag8<FM, FN>(a, acc, co0 + wm * TM, pxf, lane);
+  else epilogue_frag<FM, FN>(a, acc, co0 + wm * TM, pxf, lane);
 }
 
 // -------------------------------------------------------------------------
