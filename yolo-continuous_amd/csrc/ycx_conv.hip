@@ -1632,18 +1632,22 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
   const int tb = (int)((long long)blk * ntiles / gridDim.x), te = (int)((long long)(blk + 1) * ntiles / gridDim.x);
   if (tb >= te) return;
 
-  // second conv weights, all taps, this wave's 32 channels (A lane: co = 32 wm + 16 i + lx, k = 32 t + 8 kq ..)
+  // second conv weights, all taps, this wave's 32 channels (A lane: row lx of fragment i is channel
+  // 32 wm + 8 (lx >> 2) + 4 i + (lx & 3), k = 32 t + 8 kq ..: C rows 4 kq .. +3 of the two fragments
+  // are channels 32 wm + 8 kq .. +7, one 16-byte (e4m3: 8-byte) store per lane and pixel)
+  static_assert(FM == 2, "channel pairs");
   const __bf16* __restrict__ Wc = reinterpret_cast<const __bf16*>(ca.w);  // [Cout_pad][3][3][32]
   bf16x8 aw[9][FM];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int i = 0; i < FM; ++i)
-      aw[t][i] = *reinterpret_cast<const bf16x8*>(Wc + (size_t)(32 * wm + 16 * i + lx) * ca.Ktot + 32 * t + 8 * kq);
+      aw[t][i] = *reinterpret_cast<const bf16x8*>(Wc + (size_t)(32 * wm + 8 * (lx >> 2) + 4 * i + (lx & 3)) * ca.Ktot +
+                                                  32 * t + 8 * kq);
   f32x4 bvc[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int co = 32 * wm + 16 * i + 4 * kq;
+    const int co = 32 * wm + 8 * kq + 4 * i;
     bvc[i] = co < ca.Cout ? *reinterpret_cast<const f32x4*>(ca.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   // stem weights / bias / gather offsets (k = 8 kq + j -> tap k / 3, channel k % 3; k >= 27 gathers
@@ -1789,24 +1793,27 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[t][i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    // epilogue: bias + act, 8-byte stores (4 channels of one pixel per lane)
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int co = 32 * wm + 16 * i + 4 * kq;
-      if (co >= ca.Cout) continue;
+    // epilogue: bias (in the accumulators) + act, 8 channels of one pixel per lane
+    const int co = 32 * wm + 8 * kq;
+    if (co < ca.Cout) {  // cout % 8 == 0: the 8 channels are all valid
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int p = n * ca.HoWo + (oy0 + 2 * wn + (j >> 1)) * ca.Wo + ox0 + 16 * (j & 1) + lx;
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[4 * i + q] = act_t<ACT2>(acc[i][j][q], ca.slope);
         if constexpr (F8) {  // the stem map and this conv run in bf16; only the output is e4m3
           const float sc = ca.out_scale;
-          *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ca.y) + ca.out_coff + (size_t)p * ca.out_cs + co) =
-              f8x4_pack(act_t<ACT2>(acc[i][j][0], ca.slope) * sc, act_t<ACT2>(acc[i][j][1], ca.slope) * sc,
-                        act_t<ACT2>(acc[i][j][2], ca.slope) * sc, act_t<ACT2>(acc[i][j][3], ca.slope) * sc);
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(ca.y) + ca.out_coff + (size_t)p * ca.out_cs + co) =
+              make_uint2(f8x4_pack(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc),
+                         f8x4_pack(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc));
         } else {
-          bf16x4 ov;
+          bf16x8 ov;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) ov[q] = (__bf16)act_t<ACT2>(acc[i][j][q], ca.slope);
-          *reinterpret_cast<bf16x4*>(Y + (size_t)p * ca.out_cs + co) = ov;
+          for (int q = 0; q < 8; ++q) ov[q] = (__bf16)v[q];
+          *reinterpret_cast<bf16x8*>(Y + (size_t)p * ca.out_cs + co) = ov;
         }
       }
     }
