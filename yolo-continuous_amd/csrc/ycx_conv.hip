@@ -643,6 +643,63 @@ __device__ __forceinline__ void store4_f8(const ConvArgs& a, int p, int co, floa
   }
 }
 
+// 8 consecutive fp8 output channels of pixel p (residual added first, then scaled): 8-byte stores.
+__device__ __forceinline__ void store8_f8(const ConvArgs& a, int p, int co, float v[8]) {
+  if (a.res) {
+    const uint2 rv = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(a.res) + (size_t)p * a.res_cs +
+                                                     a.res_coff + co);
+    v[0] += __builtin_amdgcn_cvt_f32_fp8((int)rv.x, 0) * a.res_scale;
+    v[1] += __builtin_amdgcn_cvt_f32_fp8((int)rv.x, 1) * a.res_scale;
+    v[2] += __builtin_amdgcn_cvt_f32_fp8((int)rv.x, 2) * a.res_scale;
+    v[3] += __builtin_amdgcn_cvt_f32_fp8((int)rv.x, 3) * a.res_scale;
+    v[4] += __builtin_amdgcn_cvt_f32_fp8((int)rv.y, 0) * a.res_scale;
+    v[5] += __builtin_amdgcn_cvt_f32_fp8((int)rv.y, 1) * a.res_scale;
+    v[6] += __builtin_amdgcn_cvt_f32_fp8((int)rv.y, 2) * a.res_scale;
+    v[7] += __builtin_amdgcn_cvt_f32_fp8((int)rv.y, 3) * a.res_scale;
+  }
+  const float s = a.out_scale;
+  const uint2 o = make_uint2(f8x4_pack(v[0] * s, v[1] * s, v[2] * s, v[3] * s),
+                             f8x4_pack(v[4] * s, v[5] * s, v[6] * s, v[7] * s));
+  uint8_t* base = reinterpret_cast<uint8_t*>(a.y) + a.out_coff + co;
+  if (a.out_layout == YCX_OUT_NHWC_UP2) {
+    const int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    const size_t W2 = 2 * (size_t)a.Wo;
+    const size_t b0 = ((size_t)n * 2 * a.Ho + 2 * oy) * W2 + 2 * ox;
+    *reinterpret_cast<uint2*>(base + b0 * a.out_cs) = o;
+    *reinterpret_cast<uint2*>(base + (b0 + 1) * a.out_cs) = o;
+    *reinterpret_cast<uint2*>(base + (b0 + W2) * a.out_cs) = o;
+    *reinterpret_cast<uint2*>(base + (b0 + W2 + 1) * a.out_cs) = o;
+  } else {
+    *reinterpret_cast<uint2*>(base + (size_t)p * a.out_cs) = o;
+  }
+}
+
+// NHWC fp8 epilogue for permuted A rows: fragments 2k, 2k+1 hold channels cob + 32k + 8g .. +7.
+template <int FM, int FN>
+__device__ __forceinline__ void epilogue_f8x8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob, int pxb,
+                                              int lane) {
+  const float* dq = a.bias + a.Cout_pad;
+#pragma unroll
+  for (int k = 0; k < FM / 2; ++k) {
+    const int co = cob + 32 * k + 8 * (lane >> 4);
+    if (co >= a.Cout) continue;  // cout % 8 == 0
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + co), b1 = *reinterpret_cast<const f32x4*>(a.bias + co + 4);
+    const f32x4 q0 = *reinterpret_cast<const f32x4*>(dq + co), q1 = *reinterpret_cast<const f32x4*>(dq + co + 4);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int p = pxb + j * 16 + (lane & 15);
+      if (p >= a.M) continue;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = ycx_act<true>(fmaf(acc[2 * k][j][r], q0[r], b0[r]), a.act, a.slope);
+        v[4 + r] = ycx_act<true>(fmaf(acc[2 * k + 1][j][r], q1[r], b1[r]), a.act, a.slope);
+      }
+      store8_f8(a, p, co, v);
+    }
+  }
+}
+
 template <int FM, int FN>
 __device__ __forceinline__ void epilogue_f8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob, int pxb,
                                             int lane) {
@@ -708,11 +765,15 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a) {
   const int lrow = lane >> 3, pch = lane & 7;
 
   const int w_bytes = a.Cout_pad * a.Ktot, x_bytes = a.N * a.H * a.W * a.in_cs;
+  // NHWC outputs: permuted A rows as in conv_bf16_glds (8 channels, 8 bytes per lane and pixel)
+  const bool perm = a.out_layout != YCX_OUT_NCHW_F32;
   int a_off[A_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     const int row = 8 * (wid + NW * i) + lrow;
-    a_off[i] = (co0 + row) * a.Ktot + ((pch ^ swz8(row)) << 4);
+    const int f = (row % TM) >> 4, m = row & 15;
+    const int ch = perm ? (row / TM) * TM + 32 * (f >> 1) + 8 * (m >> 2) + 4 * (f & 1) + (m & 3) : row;
+    a_off[i] = (co0 + ch) * a.Ktot + ((pch ^ swz8(row)) << 4);
   }
   // swz8(8 (wid + NW i) + lrow) depends on lrow and wid & 1 only (NW even): the logical
   // chunk (so the tap select) of a lane is the same in all its slabs.
@@ -809,7 +870,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a) {
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
     __builtin_amdgcn_sched_barrier(0);
   }
-  epilogue_f8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+  static_assert(FM % 2 == 0, "fragment pairs");
+  if (perm) epilogue_f8x8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+  else epilogue_f8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
 }
 
 // -------------------------------------------------------------------------
