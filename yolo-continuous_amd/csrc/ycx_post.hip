@@ -193,7 +193,20 @@ __global__ void __launch_bounds__(256) decode_filter_kernel(DecodeFilterArgs a, 
     if (obj >= d.conf_thres) {
       float best = sigmoidf_ref(hb[(size_t)5 * hw]);
       int bi = 0;
-      for (int k = 1; k < d.nc; ++k) {
+      int k = 1;
+      // eight class logits in flight per thread (a load-use chain per class left the kernel
+      // latency-bound at ~0.8 TB/s); the compares stay in class order (first index on ties)
+      for (; k + 8 <= d.nc; k += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = hb[(size_t)(5 + k + u) * hw];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float sv = sigmoidf_ref(v[u]);
+          if (sv > best) { best = sv; bi = k + u; }
+        }
+      }
+      for (; k < d.nc; ++k) {
         float v = sigmoidf_ref(hb[(size_t)(5 + k) * hw]);
         if (v > best) { best = v; bi = k; }
       }
