@@ -62,6 +62,10 @@ def parse(argv=None):
                     help="run the N > 1 code path (process group + RCCL all-gather) even at one rank")
     ap.add_argument("--latency-steps", type=int, default=10,
                     help="unloaded latency leg: batches run one at a time (0: skip)")
+    ap.add_argument("--post-micro", action="store_true",
+                    help="fixed-load decode + NMS micro-bench on G3-recipe head logits (SURVEY 8(d)) instead of "
+                         "the network bench; prints its own JSON line")
+    ap.add_argument("--obj-shift", type=float, default=-3.0, help="--post-micro: objectness logit shift")
     return ap.parse_args(argv)
 
 
@@ -187,8 +191,97 @@ def pmc_traffic(kernel, shape):
     return round(t["per_name"][kernel]["hbm_bytes_per_launch"])
 
 
+def post_micro(args, dev):
+    """decode_box + non_max_suppression alone at a fixed load: the G3 recipe's
+    N(0, 1) head logits with the objectness logit shifted by --obj-shift (-3:
+    about 280 candidates per image at conf 0.3), [bs, 3*(5+nc), s/k, s/k] for
+    k = 32, 16, 8 (Detect order), resident in HBM; one step = ycx_decode_filter
+    + ycx_sort_nms of the batch on one stream. The CPU leg runs the oracle's
+    decode_box + non_max_suppression on the same batch. Both GPU legs are timed
+    as HIP-graph replays (10 steps per graph) so host launch cost is excluded."""
+    import ctypes
+    import numpy as np
+    from ycx import _lib as L
+    from ycx.detect import DevicePost
+    from ycx.utils.synth import synthetic_head_logits
+    bs, s = args.batch, args.size
+    shapes = [(bs, s // k, s // k) for k in (32, 16, 8)]
+    heads_cpu = synthetic_head_logits(shapes, args.nc, seed=11, obj_shift=args.obj_shift)
+    heads = [h.to(dev) for h in heads_cpu]
+    post = DevicePost(heads, args.nc, ANCHORS, MASK, (s, s), dev, args.conf, args.iou, args.max_det)
+
+    def decode_only():
+        st = L.stream_handle(dev)  # the capturing stream inside graphed()
+        post.counts.zero_()
+        L.check(L.lib.ycx_decode_filter(ctypes.byref(post.df_desc), post.heads_arr, post.cand.data_ptr(),
+                                        post.cand_rows.data_ptr(), post.counts.data_ptr(), st), "ycx_decode_filter")
+
+    def timed(fn, k):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(k):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / k
+
+    def graphed(fn, reps=10):  # host launch cost out of the timing: reps calls in one HIP graph
+        fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        return lambda: g.replay(), reps
+
+    for _ in range(args.warmup):
+        post()
+    g_post, reps = graphed(post)
+    g_dec, _ = graphed(decode_only)
+    ms = timed(g_post, args.steps) / reps
+    dec_ms = timed(g_dec, args.steps) / reps  # decode_filter + the 4-byte-per-image counts memset
+    post()
+    torch.cuda.synchronize()
+    cands = post.counts.sum().item() / bs
+    kept = post.kc.clamp(max=args.max_det).sum().item() / bs
+    rows = post.rows
+    dec_bytes = bs * rows * (args.nc + 5) * 4  # fp32 logits read once (algorithmic)
+    out = dict(metric="decode+NMS images/s at a fixed load (G3 recipe)", value=round(bs / (ms * 1e-3), 1),
+               unit="images/s", n_gpus=1, steps=args.steps, warmup=args.warmup, ms_per_step=round(ms, 4),
+               higher_is_better=True, dtype="f32", data="synthetic G3-recipe head logits",
+               config=dict(workload=f"decode_box + non_max_suppression, nc={args.nc}, {s}x{s} heads, bs={bs}, "
+                                    f"obj shift {args.obj_shift}", batch=bs, image_size=s, conf_thres=args.conf,
+                           iou_thres=args.iou, max_det=args.max_det),
+               candidates_per_image=round(cands, 1), kept_per_image=round(kept, 1),
+               roofline=dict(bound="hbm", kernel="decode_filter_kernel", achieved=round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1),
+                             peak=8000.0, unit="GB/s", frac=round(dec_bytes / (dec_ms * 1e-3) / 1e9 / 8000.0, 4),
+                             traffic=None, avg_launch_ms=round(dec_ms, 4), bytes_per_launch=dec_bytes))
+    if args.cpu_seconds > 0:
+        from oracle import ref_post
+        cores = min(16, len(os.sched_getaffinity(0)))
+        torch.set_num_threads(cores)
+        anchors = np.asarray(ANCHORS).reshape(-1, 2)
+        times = []
+        t_start = time.perf_counter()
+        while not times or (time.perf_counter() - t_start < args.cpu_seconds and len(times) < 5):
+            t0 = time.perf_counter()
+            dec = torch.cat(ref_post.decode_box(heads_cpu, anchors, MASK, args.nc, (s, s)), 1)
+            ref_post.non_max_suppression(dec, args.nc, (s, s), np.array([s, s]), True, args.conf, args.iou)
+            times.append(time.perf_counter() - t0)
+        per = statistics.median(times)
+        out["cpu_baseline"] = dict(value=round(bs / per, 2), unit="images/s", cores=cores, kind="port",
+                                   sample=f"oracle decode_box + non_max_suppression of the same {bs}-image batch, "
+                                          f"{len(times)} timed runs (median {per:.3f} s), {cores} threads")
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.post_micro:
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        return post_micro(args, dev)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

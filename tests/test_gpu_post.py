@@ -11,7 +11,8 @@ import torch
 
 from helpers import ANCHORS, MASK, g3_heads, make_model, rel_err
 from oracle import ref_forward, ref_post
-from ycx.detect import ConcurrentDetector, Detector, PipelinedDetector, decode_box, nms_device, non_max_suppression
+from ycx.detect import (ConcurrentDetector, Detector, DevicePost, PipelinedDetector, decode_box, nms_device,
+                        non_max_suppression)
 from ycx.utils.helper_io import cvt_cfg
 from ycx.utils.synth import synthetic_images
 
@@ -53,6 +54,69 @@ def test_nms_keep_rows_bit_exact(device, manifest, g3, name):
         assert k == len(gold) == e['n_keep'][b]
         np.testing.assert_array_equal(keep[b, :k].cpu().numpy(), gold)
         assert (keep[b, k:] == -1).all()
+
+
+@pytest.mark.parametrize('name', CASES)
+def test_device_post_g3(device, manifest, g3, name):
+    """DevicePost (fused ycx_decode_filter + ycx_sort_nms, the Detector's post and
+    bench.py --post-micro) on the G3 head logits vs the golden keep rows. The
+    fused filter evaluates the sigmoids on the GPU, so a candidate at the conf
+    boundary may flip by an ulp; no systematic difference is allowed."""
+    e = manifest['g3'][name]
+    heads = [h.to(device).contiguous() for h in g3_heads(e)]
+    post = DevicePost(heads, e['nc'], ANCHORS, MASK, (e['size'], e['size']), device, e['conf'], e['iou'],
+                      max_det=8192)  # nc3_dense keeps ~1.9k rows per image
+    dets, keep, kc = post()
+    torch.cuda.synchronize()
+    for b in range(e['bs']):
+        k = int(kc[b])
+        assert k <= 8192
+        want = g3[f'{name}/keep_rows/{b}']
+        got = keep[b, :k].cpu().numpy()
+        assert len(set(got.tolist()) ^ set(want.tolist())) <= max(2, len(want) // 100), (b, k, len(want))
+        assert (keep[b, k:] == -1).all()
+        assert np.isfinite(dets[b, :k].cpu().numpy()).all()
+
+
+def test_device_post_sparse_class_ties(device):
+    """Sparse waves (<= 8 candidate rows per 64) take the wave-cooperative class
+    scan in decode_filter: ties resolve to the first class (torch.max,
+    detect.py:108), a maximum past class 63 is found, and the kept rows and
+    classes equal the oracle's."""
+    nc, bs, size = 80, 2, 640
+    g = torch.Generator().manual_seed(5)
+    shapes = [(size // k, size // k) for k in (32, 16, 8)]
+    heads = [torch.randn(bs, 3, 5 + nc, h, w, generator=g) for h, w in shapes]
+    for hd in heads:
+        hd[:, :, 4] = -10.0
+    rng = np.random.default_rng(3)
+    for b in range(bs):
+        for l, hd in enumerate(heads):
+            h, w = shapes[l]
+            for t in range(12):
+                a, y, x = int(rng.integers(3)), int(rng.integers(h)), int(rng.integers(w))
+                hd[b, a, 4, y, x] = 5.0
+                kind = t % 4
+                if kind == 0:
+                    hd[b, a, 5:, y, x] = 1.5                 # all tie -> class 0
+                elif kind == 1:
+                    hd[b, a, 5:, y, x] = 0.0
+                    hd[b, a, 5 + np.array([70, 7, 3]), y, x] = 2.0   # tie -> class 3
+                elif kind == 2:
+                    hd[b, a, 5:, y, x] = -1.0
+                    hd[b, a, 5 + 79, y, x] = 3.0             # past the first 64 lanes
+    heads = [hd.reshape(bs, 3 * (5 + nc), h, w).contiguous() for hd, (h, w) in zip(heads, shapes)]
+    post = DevicePost([h.to(device) for h in heads], nc, ANCHORS, MASK, (size, size), device, 0.3, 0.45, 1000)
+    dets, keep, kc = post()
+    torch.cuda.synchronize()
+    dec = torch.cat(ref_post.decode_box(heads, A, MASK, nc, (size, size)), 1)
+    ref_keep, ref_dets = ref_post.nms_keep_rows(dec, nc, 0.3, 0.45)
+    for b in range(bs):
+        k = int(kc[b])
+        assert k == len(ref_keep[b]) > 20
+        np.testing.assert_array_equal(keep[b, :k].cpu().numpy(), ref_keep[b].numpy())
+        np.testing.assert_array_equal(dets[b, :k, 6].cpu().numpy(), ref_dets[b][:, 6].numpy())
+    assert {0, 3, 79} <= set(dets[0, :int(kc[0]), 6].cpu().long().tolist())
 
 
 @pytest.mark.parametrize('name', CASES)

@@ -180,49 +180,89 @@ __global__ void __launch_bounds__(256) decode_filter_kernel(DecodeFilterArgs a, 
   const ycx_decode_filter_desc& d = a.d;
   const int n = blockIdx.y;
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
   bool pass = false;
   ycx_cand c;
+  int l = 0, hw = 1, W = 1, H = 1, an = 0, cell = 0;
+  const float* hb = nullptr;
+  float obj = 0.0f;
   if (r < d.rows_total) {
-    int l = 0;
     while (l + 1 < d.nl && r >= d.row_off[l + 1]) ++l;
-    const int H = d.h[l], W = d.w[l], hw = H * W;
+    H = d.h[l];
+    W = d.w[l];
+    hw = H * W;
     const int local = r - d.row_off[l];
-    const int an = local / hw, cell = local - an * hw;
-    const float* hb = a.heads[l] + ((size_t)n * d.na * d.no + (size_t)an * d.no) * hw + cell;
-    const float obj = sigmoidf_ref(hb[(size_t)4 * hw]);
-    if (obj >= d.conf_thres) {
-      float best = sigmoidf_ref(hb[(size_t)5 * hw]);
-      int bi = 0;
-      int k = 1;
-      // eight class logits in flight per thread (a load-use chain per class left the kernel
-      // latency-bound at ~0.8 TB/s); the compares stay in class order (first index on ties)
-      for (; k + 8 <= d.nc; k += 8) {
-        float v[8];
+    an = local / hw;
+    cell = local - an * hw;
+    hb = a.heads[l] + ((size_t)n * d.na * d.no + (size_t)an * d.no) * hw + cell;
+    obj = sigmoidf_ref(hb[(size_t)4 * hw]);
+  }
+  // obj * cls <= obj (cls <= 1, monotone rounding): a row below conf on obj alone
+  // never passes, so its class logits are not read.
+  const bool want = hb != nullptr && obj >= d.conf_thres;
+  unsigned long long m = __ballot(want);
+  float best = 0.0f;
+  int bi = 0;
+  if (__popcll(m) <= 8) {
+    // Sparse wave (trained weights: ~1e2 candidates per image): the whole wave
+    // scans one row's classes at a time (one memory round trip for nc <= 64 per
+    // lane-class slot instead of nc / 8 per lane). The result equals the
+    // sequential strict-> scan: non-NaN maximum, first index on ties, and a NaN
+    // at class 0 sticks.
+    while (m) {
+      const int j = __ffsll(m) - 1;
+      m &= m - 1;
+      const float* hj = reinterpret_cast<const float*>(__shfl((long long)hb, j));
+      const int hwj = __shfl(hw, j);
+      float bv = 0.0f;
+      int bk = 0x7fffffff;
+      for (int k = lane; k < d.nc; k += 64) {
+        const float sv = sigmoidf_ref(hj[(size_t)(5 + k) * hwj]);
+        if (sv == sv && (bk == 0x7fffffff || sv > bv)) { bv = sv; bk = k; }
+      }
+      for (int o = 32; o; o >>= 1) {
+        const float ov = __shfl_xor(bv, o);
+        const int ok = __shfl_xor(bk, o);
+        if (ok != 0x7fffffff && (bk == 0x7fffffff || ov > bv || (ov == bv && ok < bk))) { bv = ov; bk = ok; }
+      }
+      if (lane == j) {
+        const float s0 = sigmoidf_ref(hb[(size_t)5 * hw]);
+        if (s0 != s0) { best = s0; bi = 0; } else { best = bv; bi = bk; }
+      }
+    }
+  } else if (want) {
+    best = sigmoidf_ref(hb[(size_t)5 * hw]);
+    int k = 1;
+    // eight class logits in flight per thread (a load-use chain per class left the kernel
+    // latency-bound at ~0.8 TB/s); the compares stay in class order (first index on ties)
+    for (; k + 8 <= d.nc; k += 8) {
+      float v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = hb[(size_t)(5 + k + u) * hw];
+      for (int u = 0; u < 8; ++u) v[u] = hb[(size_t)(5 + k + u) * hw];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const float sv = sigmoidf_ref(v[u]);
-          if (sv > best) { best = sv; bi = k + u; }
-        }
+      for (int u = 0; u < 8; ++u) {
+        const float sv = sigmoidf_ref(v[u]);
+        if (sv > best) { best = sv; bi = k + u; }
       }
-      for (; k < d.nc; ++k) {
-        float v = sigmoidf_ref(hb[(size_t)(5 + k) * hw]);
-        if (v > best) { best = v; bi = k; }
-      }
-      const float score = obj * best;
-      if (score >= d.conf_thres) {
-        const float gx = (float)(cell % W), gy = (float)(cell / W);
-        const float px = sigmoidf_ref(hb[0]), py = sigmoidf_ref(hb[hw]);
-        const float pw = sigmoidf_ref(hb[(size_t)2 * hw]), ph = sigmoidf_ref(hb[(size_t)3 * hw]);
-        const float bx = ((px * 2.0f) - 0.5f + gx) / (float)W;
-        const float by = ((py * 2.0f) - 0.5f + gy) / (float)H;
-        const float tw = pw * 2.0f, th = ph * 2.0f;
-        const float bw = (tw * tw * d.anchors_scaled[l][2 * an]) / (float)W;
-        const float bh = (th * th * d.anchors_scaled[l][2 * an + 1]) / (float)H;
-        pass = true;
-        c = ycx_cand{bx - bw / 2.0f, by - bh / 2.0f, bx + bw / 2.0f, by + bh / 2.0f, obj, best, bi, r};
-      }
+    }
+    for (; k < d.nc; ++k) {
+      float v = sigmoidf_ref(hb[(size_t)(5 + k) * hw]);
+      if (v > best) { best = v; bi = k; }
+    }
+  }
+  if (want) {
+    const float score = obj * best;
+    if (score >= d.conf_thres) {
+      const float gx = (float)(cell % W), gy = (float)(cell / W);
+      const float px = sigmoidf_ref(hb[0]), py = sigmoidf_ref(hb[hw]);
+      const float pw = sigmoidf_ref(hb[(size_t)2 * hw]), ph = sigmoidf_ref(hb[(size_t)3 * hw]);
+      const float bx = ((px * 2.0f) - 0.5f + gx) / (float)W;
+      const float by = ((py * 2.0f) - 0.5f + gy) / (float)H;
+      const float tw = pw * 2.0f, th = ph * 2.0f;
+      const float bw = (tw * tw * d.anchors_scaled[l][2 * an]) / (float)W;
+      const float bh = (th * th * d.anchors_scaled[l][2 * an + 1]) / (float)H;
+      pass = true;
+      c = ycx_cand{bx - bw / 2.0f, by - bh / 2.0f, bx + bw / 2.0f, by + bh / 2.0f, obj, best, bi, r};
     }
   }
   const int slot = wave_append(pass, counts + n);

@@ -196,31 +196,32 @@ def idetect_outputs(head, outs, input_hw):
     return z, xs
 
 
-class Detector:
-    """Fused device pipeline for a fixed batch shape: Model forward (static plan,
-    optionally one HIP graph) -> ycx_decode_filter -> ycx_sort_nms.
+class DevicePost:
+    """decode_box + non_max_suppression on device for fixed head shapes
+    (``detect.py:29-144``): ycx_decode_filter -> ycx_sort_nms on the current
+    stream. ``heads`` are fp32 NCHW [n, na*(5+nc), h, w] in Detect order
+    (P5, P4, P3); their storage is read at every call.
 
     Outputs stay on device: dets [n, max_det, 7] (normalised xyxy, obj,
     cls_conf, cls), keep_rows [n, max_det] (row into the concatenated
     [sum na*H*W] candidates, -1 padded), keep_counts [n] (uncapped)."""
 
-    def __init__(self, model, shape, device, anchors, anchors_mask, image_size=None, conf_thres=0.3,
-                 nms_thres=0.3, max_det=300, use_graph=True, slot=0):
-        self.model = model
-        self.engine = model.engine_for(shape, device, slot)
+    def __init__(self, heads, nc, anchors, anchors_mask, image_size, device, conf_thres=0.3, nms_thres=0.3,
+                 max_det=300):
         self.device = torch.device(device)
-        n, _, H, W = shape
-        image_size = image_size or (H, W)
-        self.x, heads = self.engine.bind_static(torch.zeros(shape, dtype=torch.float32, device=device))
-        if not isinstance(heads, list):
-            raise ValueError("ycx: Detector needs a model whose last layer is a Detect head")
+        for hd in heads:
+            _require_device(hd, "DevicePost heads")
+            if hd.dtype != torch.float32 or not hd.is_contiguous():
+                raise ValueError("ycx: DevicePost needs contiguous fp32 heads")
         self.heads = heads
-        nc = model.num_classes
+        n = heads[0].shape[0]
         d = L.DecodeFilterDesc()
         d.n, d.nl, d.na, d.no, d.nc = n, len(heads), len(anchors_mask[0]), nc + 5, nc
         off = 0
         for l, hd in enumerate(heads):
             h, w = hd.shape[2], hd.shape[3]
+            if hd.shape[0] != n or hd.shape[1] != d.na * d.no:
+                raise ValueError(f"ycx: head {l} has shape {tuple(hd.shape)}, expected [{n}, {d.na * d.no}, h, w]")
             d.h[l], d.w[l], d.row_off[l] = h, w, off
             aw, ah = _scaled_anchors(anchors, anchors_mask[l], image_size[0], h, w)
             for a in range(len(aw)):
@@ -239,11 +240,8 @@ class Detector:
         self.dets = torch.empty((n, max_det, 7), dtype=torch.float32, device=device)
         self.keep = torch.empty((n, max_det), dtype=torch.int32, device=device)
         self.kc = torch.empty((n,), dtype=torch.int32, device=device)
-        self.use_graph = use_graph
-        if use_graph:
-            self.engine.capture()
 
-    def post(self):
+    def __call__(self):
         st = L.stream_handle(self.device)
         self.counts.zero_()
         L.check(L.lib.ycx_decode_filter(ctypes.byref(self.df_desc), self.heads_arr, self.cand.data_ptr(),
@@ -252,6 +250,38 @@ class Detector:
                                    self.counts.data_ptr(), self.ws.data_ptr(), self.ws_bytes, self.dets.data_ptr(),
                                    self.keep.data_ptr(), self.kc.data_ptr(), st), "ycx_sort_nms")
         return self.dets, self.keep, self.kc
+
+
+class Detector:
+    """Fused device pipeline for a fixed batch shape: Model forward (static plan,
+    optionally one HIP graph) -> ycx_decode_filter -> ycx_sort_nms (DevicePost).
+
+    Outputs stay on device: dets [n, max_det, 7] (normalised xyxy, obj,
+    cls_conf, cls), keep_rows [n, max_det] (row into the concatenated
+    [sum na*H*W] candidates, -1 padded), keep_counts [n] (uncapped)."""
+
+    def __init__(self, model, shape, device, anchors, anchors_mask, image_size=None, conf_thres=0.3,
+                 nms_thres=0.3, max_det=300, use_graph=True, slot=0):
+        self.model = model
+        self.engine = model.engine_for(shape, device, slot)
+        self.device = torch.device(device)
+        n, _, H, W = shape
+        image_size = image_size or (H, W)
+        self.x, heads = self.engine.bind_static(torch.zeros(shape, dtype=torch.float32, device=device))
+        if not isinstance(heads, list):
+            raise ValueError("ycx: Detector needs a model whose last layer is a Detect head")
+        self.heads = heads
+        self._post = DevicePost(heads, model.num_classes, anchors, anchors_mask, image_size, device, conf_thres,
+                                nms_thres, max_det)
+        for k in ("rows", "df_desc", "cand", "cand_rows", "counts", "nms_desc", "ws_bytes", "ws", "dets", "keep",
+                  "kc"):
+            setattr(self, k, getattr(self._post, k))
+        self.use_graph = use_graph
+        if use_graph:
+            self.engine.capture()
+
+    def post(self):
+        return self._post()
 
     def forward(self, events=None):
         """The model forward on the static input buffer (current stream)."""
