@@ -56,12 +56,15 @@ def test_nms_keep_rows_bit_exact(device, manifest, g3, name):
         assert (keep[b, k:] == -1).all()
 
 
+@pytest.mark.parametrize('scalar', [False, True])
 @pytest.mark.parametrize('name', CASES)
-def test_device_post_g3(device, manifest, g3, name):
+def test_device_post_g3(device, manifest, g3, name, scalar, monkeypatch):
     """DevicePost (fused ycx_decode_filter + ycx_sort_nms, the Detector's post and
     bench.py --post-micro) on the G3 head logits vs the golden keep rows. The
     fused filter evaluates the sigmoids on the GPU, so a candidate at the conf
     boundary may flip by an ulp; no systematic difference is allowed."""
+    if scalar:  # the one-row-per-thread kernel (heads with h*w % 4 != 0 or unaligned take it)
+        monkeypatch.setenv('YCX_DECODE_SCALAR', '1')
     e = manifest['g3'][name]
     heads = [h.to(device).contiguous() for h in g3_heads(e)]
     post = DevicePost(heads, e['nc'], ANCHORS, MASK, (e['size'], e['size']), device, e['conf'], e['iou'],
@@ -78,11 +81,14 @@ def test_device_post_g3(device, manifest, g3, name):
         assert np.isfinite(dets[b, :k].cpu().numpy()).all()
 
 
-def test_device_post_sparse_class_ties(device):
-    """Sparse waves (<= 8 candidate rows per 64) take the wave-cooperative class
-    scan in decode_filter: ties resolve to the first class (torch.max,
+@pytest.mark.parametrize('scalar', [False, True])
+def test_device_post_sparse_class_ties(device, scalar, monkeypatch):
+    """Sparse rows through both decode_filter kernels (four rows per thread; one
+    row per thread with the wave-cooperative class scan for <= 8 rows per wave): ties resolve to the first class (torch.max,
     detect.py:108), a maximum past class 63 is found, and the kept rows and
     classes equal the oracle's."""
+    if scalar:
+        monkeypatch.setenv('YCX_DECODE_SCALAR', '1')
     nc, bs, size = 80, 2, 640
     g = torch.Generator().manual_seed(5)
     shapes = [(size // k, size // k) for k in (32, 16, 8)]

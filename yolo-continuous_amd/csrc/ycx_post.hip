@@ -11,6 +11,8 @@
 // contraction is disabled for this file so every product/sum rounds like the
 // CPU code does.
 #pragma clang fp contract(off)
+#include <stdlib.h>
+#include <stdint.h>
 #include "ycx_internal.h"
 
 namespace {
@@ -272,6 +274,161 @@ __global__ void __launch_bounds__(256) decode_filter_kernel(DecodeFilterArgs a, 
   }
 }
 
+// Four consecutive rows (cells of one level/anchor plane) per thread: every
+// class plane is read with 16-byte loads, so a wave streams 1 KB runs of each
+// plane instead of 256 B (the fp32 NCHW heads put a row's nc logits in nc
+// planes). Same float ops per row as decode_filter_kernel. Needs h*w % 4 == 0
+// on every level and 16-byte aligned heads (checked by the launcher).
+__global__ void __launch_bounds__(256) decode_filter4_kernel(DecodeFilterArgs a, ycx_cand* __restrict__ cand,
+                                                             int* __restrict__ rows_out, int* __restrict__ counts) {
+  const ycx_decode_filter_desc& d = a.d;
+  const int n = blockIdx.y;
+  const int r0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int lane = threadIdx.x & 63;
+  bool pass[4] = {false, false, false, false};
+  ycx_cand c[4];
+  int l = 0, H = 1, W = 1, hw = 4, an = 0, cell = 0;
+  const float* hb = nullptr;
+  float obj[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  bool want[4] = {false, false, false, false};
+  if (r0 < d.rows_total) {
+    while (l + 1 < d.nl && r0 >= d.row_off[l + 1]) ++l;
+    H = d.h[l];
+    W = d.w[l];
+    hw = H * W;
+    const int local = r0 - d.row_off[l];
+    an = local / hw;
+    cell = local - an * hw;
+    hb = a.heads[l] + ((size_t)n * d.na * d.no + (size_t)an * d.no) * hw + cell;
+    const float4 o = *reinterpret_cast<const float4*>(hb + (size_t)4 * hw);
+    const float ov[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      obj[i] = sigmoidf_ref(ov[i]);
+      want[i] = obj[i] >= d.conf_thres;  // obj * cls <= obj: otherwise the row cannot pass
+    }
+  }
+  unsigned long long wm[4];
+  int nwant = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    wm[i] = __ballot(want[i]);
+    nwant += __popcll(wm[i]);
+  }
+  float best[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  int bi[4] = {0, 0, 0, 0};
+  const bool any = want[0] || want[1] || want[2] || want[3];
+  auto plane = [&](int ch) { return *reinterpret_cast<const float4*>(hb + (size_t)ch * hw); };
+  if (nwant <= 8) {
+    // Sparse wave (trained weights: ~1e2 candidates per image): the whole wave
+    // scans one row's classes at a time, one memory round trip instead of nc / 4.
+    // The wave argmax equals the sequential strict-> scan: non-NaN maximum, first
+    // index on ties, and a NaN at class 0 sticks.
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      unsigned long long m = wm[i];
+      while (m) {
+        const int j = __ffsll(m) - 1;
+        m &= m - 1;
+        const float* hj = reinterpret_cast<const float*>(__shfl((long long)hb, j)) + i;
+        const int hwj = __shfl(hw, j);
+        float bv = 0.0f;
+        int bk = 0x7fffffff;
+        for (int k = lane; k < d.nc; k += 64) {
+          const float sv = sigmoidf_ref(hj[(size_t)(5 + k) * hwj]);
+          if (sv == sv && (bk == 0x7fffffff || sv > bv)) { bv = sv; bk = k; }
+        }
+        for (int o = 32; o; o >>= 1) {
+          const float ov = __shfl_xor(bv, o);
+          const int ok = __shfl_xor(bk, o);
+          if (ok != 0x7fffffff && (bk == 0x7fffffff || ov > bv || (ov == bv && ok < bk))) { bv = ov; bk = ok; }
+        }
+        if (lane == j) {
+          const float s0 = sigmoidf_ref(hb[(size_t)5 * hw + i]);
+          if (s0 != s0) { best[i] = s0; bi[i] = 0; } else { best[i] = bv; bi[i] = bk; }
+        }
+      }
+    }
+  } else if (any) {
+    const float4 c0 = plane(5);
+    best[0] = sigmoidf_ref(c0.x);
+    best[1] = sigmoidf_ref(c0.y);
+    best[2] = sigmoidf_ref(c0.z);
+    best[3] = sigmoidf_ref(c0.w);
+    {
+      int k = 1;
+      for (; k + 4 <= d.nc; k += 4) {  // 16 logits in flight; compares in class order (first index on ties)
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = plane(5 + k + u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float sv = sigmoidf_ref(e[i]);
+            if (sv > best[i]) { best[i] = sv; bi[i] = k + u; }
+          }
+        }
+      }
+      for (; k < d.nc; ++k) {
+        const float4 v = plane(5 + k);
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float sv = sigmoidf_ref(e[i]);
+          if (sv > best[i]) { best[i] = sv; bi[i] = k; }
+        }
+      }
+    }
+  }
+  if (any) {
+    {
+      const float4 b0 = plane(0), b1 = plane(1), b2 = plane(2), b3 = plane(3);
+      const float lx[4] = {b0.x, b0.y, b0.z, b0.w}, ly[4] = {b1.x, b1.y, b1.z, b1.w};
+      const float lw[4] = {b2.x, b2.y, b2.z, b2.w}, lh[4] = {b3.x, b3.y, b3.z, b3.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float score = obj[i] * best[i];
+        if (want[i] && score >= d.conf_thres) {
+          const int ci = cell + i;
+          const float gx = (float)(ci % W), gy = (float)(ci / W);
+          const float px = sigmoidf_ref(lx[i]), py = sigmoidf_ref(ly[i]);
+          const float pw = sigmoidf_ref(lw[i]), ph = sigmoidf_ref(lh[i]);
+          const float bx = ((px * 2.0f) - 0.5f + gx) / (float)W;
+          const float by = ((py * 2.0f) - 0.5f + gy) / (float)H;
+          const float tw = pw * 2.0f, th = ph * 2.0f;
+          const float bw = (tw * tw * d.anchors_scaled[l][2 * an]) / (float)W;
+          const float bh = (th * th * d.anchors_scaled[l][2 * an + 1]) / (float)H;
+          pass[i] = true;
+          c[i] = ycx_cand{bx - bw / 2.0f, by - bh / 2.0f, bx + bw / 2.0f, by + bh / 2.0f, obj[i], best[i], bi[i],
+                          r0 + i};
+        }
+      }
+    }
+  }
+  // Wave-aggregated append of up to 4 rows per lane (rows stay ascending within the wave).
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int tot = 0, pre = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned long long m = __ballot(pass[i]);
+    tot += __popcll(m);
+    pre += __popcll(m & lt);
+  }
+  if (tot == 0) return;  // wave-uniform
+  int base = 0;
+  if (lane == 0) base = atomicAdd(counts + n, tot);
+  int slot = __shfl(base, 0) + pre;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (pass[i]) {
+      cand[(size_t)n * d.rows_total + r0 + i] = c[i];
+      rows_out[(size_t)n * d.rows_total + slot++] = r0 + i;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" ycx_status ycx_decode(const ycx_decode_desc* d, const float* head, float* out, void* stream) {
@@ -322,8 +479,17 @@ extern "C" ycx_status ycx_decode_filter(const ycx_decode_filter_desc* d, const f
   DecodeFilterArgs a;
   a.d = *d;
   for (int l = 0; l < 4; ++l) a.heads[l] = l < d->nl ? heads[l] : nullptr;
-  dim3 grid(ycx_cdiv(d->rows_total, 256), d->n);
-  hipLaunchKernelGGL(decode_filter_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a, cand,
-                     cand_rows, cand_counts);
+  bool quad = getenv("YCX_DECODE_SCALAR") == nullptr;  // A/B switch
+  for (int l = 0; l < d->nl; ++l)
+    quad = quad && (d->h[l] * d->w[l]) % 4 == 0 && (reinterpret_cast<uintptr_t>(heads[l]) & 15) == 0;
+  if (quad) {
+    dim3 grid(ycx_cdiv(d->rows_total / 4, 256), d->n);
+    hipLaunchKernelGGL(decode_filter4_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a, cand,
+                       cand_rows, cand_counts);
+  } else {
+    dim3 grid(ycx_cdiv(d->rows_total, 256), d->n);
+    hipLaunchKernelGGL(decode_filter_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a, cand,
+                       cand_rows, cand_counts);
+  }
   return ycx_launch_status();
 }
