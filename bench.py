@@ -56,7 +56,10 @@ def parse(argv=None):
     ap.add_argument("--conf", type=float, default=0.3)
     ap.add_argument("--iou", type=float, default=0.3)
     ap.add_argument("--max-det", type=int, default=300)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample (0: skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="0: skip the CPU baseline; --post-micro: time budget of its CPU leg")
+    ap.add_argument("--cpu-batch", type=int, default=32, help="CPU baseline batch (BASELINE.md §4: 32)")
+    ap.add_argument("--cpu-iters", type=int, default=3, help="CPU baseline timed iterations (after 1 warm-up)")
     ap.add_argument("--roofline-steps", type=int, default=3)
     ap.add_argument("--dist", action="store_true",
                     help="run the N > 1 code path (process group + RCCL all-gather) even at one rank")
@@ -113,36 +116,70 @@ def roofline(det, steps, precision):
                             for k, v in sorted(per.items(), key=lambda kv: -kv[1]['ms'])})
 
 
-def cpu_baseline(args, sd, model_cfg, budget_s):
-    """The oracle (CPU fp32 restatement of the reference path: forward + decode_box
-    + non_max_suppression) on a bounded sample of the same workload."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _cgroup_cpus():
+    """CPUs granted by the cgroup quota (cpu.max), or None when unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(args, sd, model_cfg):
+    """the oracle (CPU fp32 restatement of the reference path:
+    forward + decode_box + non_max_suppression, torch.no_grad, eval) on the
+    bench's own workload shape (yolov7 nc=80, bs=32 at 640x640, seeded U[0,1)
+    images), 1 warm-up + 3 timed iterations, with
+    torch.set_num_threads(len(os.sched_getaffinity(0))) -- capped at the cgroup
+    CPU quota when one is set, since threads past the quota only time-slice."""
     import numpy as np
     from oracle import ref_forward, ref_post
     from ycx.utils.synth import synthetic_images
-    cores = min(16, len(os.sched_getaffinity(0)))
-    torch.set_num_threads(cores)
+    affinity = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpus()
+    threads = min(affinity, quota) if quota else affinity
+    torch.set_num_threads(threads)
     fwd = ref_forward.build(model_cfg, ANCHORS, args.nc, sd)
     anchors = np.asarray(ANCHORS).reshape(-1, 2)
-    n = 2
-    x = synthetic_images(n, 3, args.size, args.size, seed=1)
+    n = args.cpu_batch
+    x = synthetic_images(n, 3, args.size, args.size, seed=1000)
 
     def one():
-        heads = fwd(x)
-        dec = torch.cat(ref_post.decode_box(heads, anchors, MASK, args.nc, (args.size, args.size)), 1)
-        ref_post.non_max_suppression(dec, args.nc, (args.size, args.size), np.array([args.size, args.size]), True,
-                                     args.conf, args.iou)
+        with torch.no_grad():
+            heads = fwd(x)
+            dec = torch.cat(ref_post.decode_box(heads, anchors, MASK, args.nc, (args.size, args.size)), 1)
+            ref_post.non_max_suppression(dec, args.nc, (args.size, args.size), np.array([args.size, args.size]),
+                                         True, args.conf, args.iou)
     one()  # warm-up
     times = []
-    t_start = time.perf_counter()
-    while not times or (time.perf_counter() - t_start < budget_s and len(times) < 5):
+    for _ in range(args.cpu_iters):
         t0 = time.perf_counter()
         one()
         times.append(time.perf_counter() - t0)
     per_batch = statistics.median(times)
-    return dict(value=round(n / per_batch, 4), unit="images/s", cores=cores, kind="port",
-                sample=f"oracle forward+decode+NMS, {n} images {args.size}x{args.size} per batch, "
-                       f"{len(times)} timed batches (median {per_batch:.2f} s) + 1 warm-up, fp32, "
-                       f"torch {torch.__version__} CPU, {cores} threads")
+    model = _cpu_model()
+    return dict(value=round(n / per_batch, 4), unit="images/s", cores=threads, threads=threads,
+                affinity_cpus=affinity, cgroup_cpus=quota, cpu_model=model, batch=n, kind="port",
+                p50_batch_s=round(per_batch, 3), iterations=args.cpu_iters, warmup=1,
+                sample=f"oracle forward + decode_box + non_max_suppression (fp32, eval, no_grad; C greedy NMS "
+                       f"restatement), yolov7 nc={args.nc}, {n} images {args.size}x{args.size} per batch, "
+                       f"1 warm-up + {args.cpu_iters} timed batches (p50 {per_batch:.2f} s), {threads} threads "
+                       f"(affinity {affinity}, cgroup quota {quota}), {model}, torch {torch.__version__}")
 
 
 def setup(args, dev, rank=0, use_graph=None, pipeline=False):
@@ -366,7 +403,7 @@ def main():
     rl = roofline(det1, args.roofline_steps, args.precision) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(args, sd, cfg, args.cpu_seconds)
+        cpu = cpu_baseline(args, sd, cfg)
     if rank == 0:
         peak = PEAK[args.precision]
         out = {
@@ -385,7 +422,7 @@ def main():
                        "latency": "p50_ms: submit -> detections of a batch in the timed loop (batches_in_flight "
                                   "queued); p50_ms_unloaded: host wall time of one batch alone, synchronised",
                        "conf_thres": args.conf, "iou_thres": args.iou, "max_det": args.max_det},
-            "mfma_fraction_whole_step": round(model.engine_for(shape, dev).flops_per_image * value /
+            "mfma_fraction_whole_step": round(det1.engine.flops_per_image * value /
                                               (world * peak * 1e12), 4),
             "roofline": {"bound": "mfma", "kernel": rl['kernel'], "achieved": round(rl['achieved'], 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(rl['achieved'] / peak, 4),

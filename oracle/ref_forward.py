@@ -14,6 +14,7 @@ runs it with the same ATen op sequence as the reference modules in eval mode:
   Detect   [conv_P5(x2), conv_P4(x1), conv_P3(x0)] nets/detect.py:27-38
   IDetect  raw (bs, na, ny, nx, no) maps           nets/idetect.py:26-32 (training-mode view;
                                                    the reference's eval branch crashes)
+  IAuxDetect main heads only (eval discards m2)    nets/iaux_detect.py:27-49
 
 The channel bookkeeping restates parse_model (nets/yolo.py:15-87). Layer
 execution restates the interpreter loop (nets/yolo.py:143-153).
@@ -126,6 +127,9 @@ def build(cfg: dict, anchors, num_classes: int, state_dict: dict, image_chan: in
             return x
         return run_module(L['m'], L['args'], L['p'], x)
 
+    # the save list (nets/yolo.py:82, 151): only outputs a later layer reads are kept
+    save = {j % L['i'] for L in layers for j in ([L['f']] if isinstance(L['f'], int) else L['f']) if j != -1}
+
     def forward(x):
         y = []
         with torch.no_grad():
@@ -134,7 +138,7 @@ def build(cfg: dict, anchors, num_classes: int, state_dict: dict, image_chan: in
                 if f != -1:
                     x = y[f] if isinstance(f, int) else [x if j == -1 else y[j] for j in f]
                 x = run_layer(L, x)
-                y.append(x)
+                y.append(x if L['i'] in save else None)
         return x
 
     return forward
@@ -223,9 +227,10 @@ def run_module(m, args, p: _P, x):
         out1 = F.conv2d(x[1], p('yolo_head_P4.weight'), p('yolo_head_P4.bias'))
         out2 = F.conv2d(x[0], p('yolo_head_P3.weight'), p('yolo_head_P3.bias'))
         return [out0, out1, out2]
-    if m == 'IDetect':
+    if m in ('IDetect', 'IAuxDetect'):  # IAuxDetect eval: main heads on x[:nl] (nets/iaux_detect.py:28-31, 49)
         outs = []
-        for i in range(len(x)):
+        nl = len(x) if m == 'IDetect' else len(x) // 2
+        for i in range(nl):
             xi = p(f'ia.{i}.implicit') + x[i]
             xi = F.conv2d(xi, p(f'm.{i}.weight'), p(f'm.{i}.bias'))
             outs.append(p(f'im.{i}.implicit') * xi)

@@ -13,12 +13,50 @@ nms                     torchvision.ops.nms as called at detect.py:133 — torch
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import numpy as np
 import torch
 
+_C_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_c", "libycx_oracle.so")
+_c = None
+
+
+def _clib():
+    """oracle/nms_ref.c (built by __graft_entry__.build() / oracle/Makefile), or None."""
+    global _c
+    if _c is None:
+        _c = False
+        if os.path.exists(_C_LIB):
+            lib = ctypes.CDLL(_C_LIB)
+            lib.ycx_oracle_nms.restype = ctypes.c_int64
+            lib.ycx_oracle_nms.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_double,
+                                           ctypes.c_void_p]
+            _c = lib
+    return _c or None
+
 
 def nms(boxes, scores, iou_threshold):
-    """torchvision.ops.nms restated (CPU algorithm): int64 keep indices, score-descending."""
+    """torchvision.ops.nms restated (CPU algorithm): int64 keep indices,
+    score-descending. Runs the C restatement (oracle/nms_ref.c, the same float32
+    operations; tests/test_oracle_golden.py checks the two agree) when it is
+    built, else the numpy one below."""
+    lib = _clib()
+    if lib is None:
+        return nms_numpy(boxes, scores, iou_threshold)
+    b = np.ascontiguousarray(boxes.detach().cpu().numpy(), dtype=np.float32)
+    s = np.ascontiguousarray(scores.detach().cpu().numpy(), dtype=np.float32)
+    n = b.shape[0]
+    keep = np.empty((max(n, 1),), dtype=np.int64)
+    k = lib.ycx_oracle_nms(b.ctypes.data, s.ctypes.data, n, float(iou_threshold), keep.ctypes.data)
+    if k < 0:
+        raise MemoryError("oracle nms")
+    return torch.from_numpy(keep[:k].copy())
+
+
+def nms_numpy(boxes, scores, iou_threshold):
+    """torchvision.ops.nms restated in numpy (the reference form of the oracle)."""
     b = boxes.detach().cpu().numpy().astype(np.float32, copy=False)
     s = scores.detach().cpu().numpy().astype(np.float32, copy=False)
     n = b.shape[0]

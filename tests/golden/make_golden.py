@@ -105,17 +105,34 @@ def mini_nets():
                      [[[1, 2, 3], 1, 'Detect', ['nc', 'anchors']]]), 3),
         'idetect': (d([stem(), [-1, 1, 'Conv', [64, 3, 2]], [-1, 1, 'Conv', [128, 3, 2]], [-1, 1, 'Conv', [256, 3, 2]]],
                       [[[1, 2, 3], 1, 'IDetect', ['nc', 'anchors']]]), 3),
+        # round 2 (appended: seeds follow the position): an upsample that cannot fuse into its
+        # producer (a pool) lands in the middle of a concat buffer (channel offset 32)
+        'upsample_offset': (d([stem(), [-1, 1, 'Conv', [64, 3, 2]], [-1, 1, 'MP', []],
+                               [-1, 1, 'nn.Upsample', ['None', 2, 'nearest']], [0, 1, 'Conv', [32, 3, 2]],
+                               [[-1, -2, 1], 1, 'Concat', [1]], [-1, 1, 'Conv', [64, 1, 1]]]), 3),
+        # IAuxDetect (nets/iaux_detect.py): main heads on layers 1-3, aux heads on 4-6; eval output
+        # with the strides set on the module (its stride is None, like IDetect's)
+        'iauxdetect': (d([stem(), [-1, 1, 'Conv', [64, 3, 2]], [-1, 1, 'Conv', [128, 3, 2]],
+                          [-1, 1, 'Conv', [256, 3, 2]], [1, 1, 'Conv', [64, 1, 1]], [2, 1, 'Conv', [128, 1, 1]],
+                          [3, 1, 'Conv', [256, 1, 1]]],
+                         [[[1, 2, 3, 4, 5, 6], 1, 'IAuxDetect', ['nc', 'anchors']]]), 3),
     }
 
+AUX_STRIDES = [2.0, 4.0, 8.0]  # 24 / (12, 6, 3), as the build derives them
 
-def run_ref(Model, cfg, nc, x, seed, idetect_raw=False):
+
+def run_ref(Model, cfg, nc, x, seed, idetect_raw=False, strides=None):
     m = Model(cfg, ANCHORS, nc).eval()
     sd = synthetic_state_dict(m, seed=seed)
     m.load_state_dict(sd)
     if idetect_raw:  # the reference's IDetect eval branch crashes (stride=None): take the raw maps
         m.model[-1].training = True
+    if strides is not None:  # eval branch with the strides set on the head (nothing else touched)
+        m.model[-1].stride = torch.tensor(strides)
     with torch.no_grad():
         y = m(x)
+    if strides is not None:  # (cat(z, 1), x[:nl]) -> [z, x0, x1, ...]
+        y = [y[0]] + list(y[1])
     ys = y if isinstance(y, (list, tuple)) else [y]
     return [t.detach().numpy().copy() for t in ys], sd_hash(sd), len(sd)
 
@@ -142,8 +159,38 @@ def make_idetect_eval(Model, manifest):
     print('G4 idetect_eval', z.shape, [t.shape for t in xs])
 
 
+def add_g1(Model, names):
+    """Append G1 cases (by name) to an existing g1_ops.npz / manifest; the seeds
+    come from the case's position in mini_nets(), exactly as a full run sets them."""
+    with open(os.path.join(GOLD, 'manifest.json')) as f:
+        manifest = json.load(f)
+    g1 = dict(np.load(os.path.join(GOLD, 'g1_ops.npz')))
+    nets = list(mini_nets().items())
+    for i, (name, (cfg, nc)) in enumerate(nets):
+        if name not in names:
+            continue
+        x = synthetic_images(2, 3, 24, 24, seed=100 + i)
+        strides = AUX_STRIDES if name == 'iauxdetect' else None
+        outs, h, nkeys = run_ref(Model, cfg, nc, x, seed=i, idetect_raw=(name == 'idetect'), strides=strides)
+        for k in [k for k in g1 if k.startswith(name + '/')]:
+            del g1[k]
+        for j, o in enumerate(outs):
+            g1[f'{name}/{j}'] = o
+        manifest['g1'][name] = dict(cfg=cfg, nc=nc, shape=[2, 3, 24, 24], img_seed=100 + i, w_seed=i,
+                                    sd_hash=h, n_keys=nkeys, n_out=len(outs))
+        if strides is not None:
+            manifest['g1'][name]['strides'] = strides
+        print('G1+', name, [o.shape for o in outs])
+    np.savez(os.path.join(GOLD, 'g1_ops.npz'), **g1)
+    with open(os.path.join(GOLD, 'manifest.json'), 'w') as f:
+        json.dump(manifest, f, indent=1)
+
+
 def main():
     Model, detect, cvt_cfg = import_reference()
+    if len(sys.argv) > 2 and sys.argv[1] == 'g1add':  # append named G1 cases only
+        add_g1(Model, sys.argv[2:])
+        return
     if len(sys.argv) > 1 and sys.argv[1] == 'g4':  # add only the IDetect-eval fixture
         with open(os.path.join(GOLD, 'manifest.json')) as f:
             manifest = json.load(f)
@@ -163,11 +210,14 @@ def main():
     g1 = {}
     for i, (name, (cfg, nc)) in enumerate(mini_nets().items()):
         x = synthetic_images(2, 3, 24, 24, seed=100 + i)
-        outs, h, nkeys = run_ref(Model, cfg, nc, x, seed=i, idetect_raw=(name == 'idetect'))
+        strides = AUX_STRIDES if name == 'iauxdetect' else None
+        outs, h, nkeys = run_ref(Model, cfg, nc, x, seed=i, idetect_raw=(name == 'idetect'), strides=strides)
         for j, o in enumerate(outs):
             g1[f'{name}/{j}'] = o
         manifest['g1'][name] = dict(cfg=cfg, nc=nc, shape=[2, 3, 24, 24], img_seed=100 + i, w_seed=i,
                                     sd_hash=h, n_keys=nkeys, n_out=len(outs))
+        if strides is not None:
+            manifest['g1'][name]['strides'] = strides
         print('G1', name, [o.shape for o in outs])
     np.savez(os.path.join(GOLD, 'g1_ops.npz'), **g1)
 

@@ -85,3 +85,23 @@ def test_gather_world2_gloo(global_batch):
             assert o is None
         else:
             assert o.dtype == np.float32 and o.shape == (k, 7) and o[0, 0] == g
+
+
+def test_to_output_list_truncation_is_explicit():
+    """count > max_det: the list holds max_det rows for that image, and the
+    result says so (raw counts + truncated flags + a warning), never a silent
+    slice that disagrees with the count."""
+    max_det = 4
+    dets = torch.arange(3 * max_det * 7, dtype=torch.float32).reshape(3, max_det, 7)
+    counts = torch.tensor([2, 9, 0], dtype=torch.int32)
+    with pytest.warns(RuntimeWarning, match="truncated"):
+        out = to_output_list(dets, counts)
+    assert out[0].shape == (2, 7) and out[1].shape == (max_det, 7) and out[2] is None
+    assert out.truncated == [False, True, False] and out.any_truncated
+    assert out.counts.tolist() == [2, 9, 0]
+    np.testing.assert_array_equal(out[1], dets[1].numpy())
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        ok = to_output_list(dets, torch.tensor([1, 4, 0], dtype=torch.int32))
+    assert not ok.any_truncated and ok[1].shape == (4, 7)

@@ -18,7 +18,8 @@ pytestmark = pytest.mark.gpu
 
 F32_TOL, BF16_TOL = 1e-3, 5e-2
 G1_NAMES = ['conv_k3s1_cin32', 'conv_k3s2_cin32', 'conv_k1_cin64', 'conv_leaky', 'stem_s2_leaky', 'pools',
-            'upsample_concat', 'upsample_shared', 'sppcspc', 'repconv', 'csp_blocks', 'detect', 'idetect']
+            'upsample_concat', 'upsample_shared', 'sppcspc', 'repconv', 'csp_blocks', 'detect', 'idetect',
+            'upsample_offset', 'iauxdetect']
 
 
 def _outs(y):
@@ -41,6 +42,10 @@ def test_g1_ops(device, manifest, g1, name, precision, tol):
         z_ref, _ = ref_post.idetect_eval(gold_nchw, head.anchors.cpu().view(len(y), -1).tolist(), head.na, head.no,
                                          strides)
         assert z.shape == z_ref.shape and rel_err(z.cpu(), z_ref) < tol, ('z', rel_err(z.cpu(), z_ref))
+    if name == 'iauxdetect':  # eval branch (z, x[:nl]) vs the reference's own eval output, strides set
+        z, xs = y
+        assert [x.shape[2] / o.shape[2] for o in xs] == e['strides']
+        y = [z] + list(xs)
     outs = _outs(y)
     assert len(outs) == e['n_out']
     for j, o in enumerate(outs):

@@ -1,0 +1,23 @@
+"""Host-side helpers against the oracle (CPU only, no GPU calls)."""
+import numpy as np
+import pytest
+
+from oracle import ref_post
+from ycx.detect import yolo_correct_boxes
+
+
+@pytest.mark.parametrize('letterbox', [True, False])
+@pytest.mark.parametrize('image_hw', [(512, 773), (640, 640), (1080, 1920), (333, 17)])
+def test_yolo_correct_boxes_matches_oracle(letterbox, image_hw):
+    """The host yolo_correct_boxes (detect.py:147-165) reproduces the reference's
+    numpy arithmetic bit for bit, including the in-place float32 scaling of the
+    caller's box_wh."""
+    rng = np.random.default_rng(sum(image_hw) + letterbox)
+    xy = rng.random((257, 2), dtype=np.float32)
+    wh = rng.random((257, 2), dtype=np.float32) * np.float32(0.5)
+    wh_a, wh_b = wh.copy(), wh.copy()
+    got = yolo_correct_boxes(xy.copy(), wh_a, (640, 640), np.array(image_hw), letterbox)
+    want = ref_post.yolo_correct_boxes(xy.copy(), wh_b, (640, 640), np.array(image_hw), letterbox)
+    assert got.dtype == want.dtype and got.shape == want.shape == (257, 4)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(wh_a, wh_b)  # the same in-place side effect on the caller's array

@@ -15,7 +15,8 @@ from ycx.utils.helper_io import cvt_cfg
 from ycx.utils.synth import synthetic_images
 
 G1_NAMES = ['conv_k3s1_cin32', 'conv_k3s2_cin32', 'conv_k1_cin64', 'conv_leaky', 'stem_s2_leaky', 'pools',
-            'upsample_concat', 'upsample_shared', 'sppcspc', 'repconv', 'csp_blocks', 'detect', 'idetect']
+            'upsample_concat', 'upsample_shared', 'sppcspc', 'repconv', 'csp_blocks', 'detect', 'idetect',
+            'upsample_offset', 'iauxdetect']
 
 
 def _close(a, b):
@@ -32,6 +33,9 @@ def test_oracle_g1(manifest, g1, name):
     fwd = ref_forward.build(e['cfg'], ANCHORS, e['nc'], sd)
     out = fwd(x)
     outs = out if isinstance(out, list) else [out]
+    if name == 'iauxdetect':  # the fixture is the reference's eval output [z, x0, x1, x2], strides set
+        z, xs = ref_post.idetect_eval(outs, ANCHORS, 3, e['nc'] + 5, e['strides'])
+        outs = [z] + xs
     assert len(outs) == e['n_out']
     for j, o in enumerate(outs):
         gold = g1[f'{name}/{j}']
@@ -109,3 +113,25 @@ def test_oracle_idetect_eval(manifest):
     assert len(xs) == e['n_x']
     for j, t in enumerate(xs):
         _close(t.numpy(), g4[f'idetect_eval/x{j}'])
+
+
+@pytest.mark.parametrize('seed', [0, 1, 2])
+def test_oracle_c_nms_equals_numpy(seed):
+    """oracle/nms_ref.c (the fast restatement bench.py's CPU baseline and the
+    big-batch tests run) == the numpy restatement, on dense overlapping boxes
+    with exact score ties, zero-area boxes and duplicates."""
+    from oracle.ref_post import _clib, nms, nms_numpy
+    assert _clib() is not None, "oracle C library not built (python -c 'import __graft_entry__ as g; g.build()')"
+    g = torch.Generator().manual_seed(seed)
+    n = 3000
+    xy = torch.rand(n, 2, generator=g) * 50
+    wh = torch.rand(n, 2, generator=g) * 20
+    boxes = torch.cat([xy, xy + wh], 1)
+    boxes[::97, 2:] = boxes[::97, :2]             # zero-area boxes
+    boxes[1::53] = boxes[0::53][:boxes[1::53].shape[0]]  # exact duplicates
+    scores = (torch.rand(n, generator=g) * 64).floor() / 64  # many exact ties
+    for thr in (0.3, 0.45, 0.7):
+        a = nms(boxes, scores, thr)
+        b = nms_numpy(boxes, scores, thr)
+        assert torch.equal(a, b), (thr, len(a), len(b))
+    assert len(nms(boxes[:0], scores[:0], 0.5)) == 0

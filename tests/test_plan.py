@@ -124,3 +124,29 @@ def test_prepack_file_format_checks(tmp_path):
     m, _ = make_model('yolov7-tiny', 1, 0)
     h = prepack.state_dict_sha256(m)
     assert h == prepack.state_dict_sha256(m) and len(h) == 64
+
+
+def test_unfused_upsample_writes_its_concat_slice(manifest):
+    """An upsample that cannot fuse (its producer is a pool) and lands in the
+    middle of a concat buffer keeps that channel offset (the copy
+    used offset 0 and overwrote the first concat input)."""
+    e = manifest['g1']['upsample_offset']
+    m = Model(e['cfg'], ANCHORS, e['nc'])
+    plan = Plan(m, tuple(e['shape']))
+    ups = [nd for nd in plan.graph.nodes if nd.kind == 'up']
+    assert len(ups) == 1 and ups[0].out.coff == 32 and ups[0].out.buf.c == 160
+    assert plan.counts().get('up') == 1
+
+
+def test_iauxdetect_lowers_main_heads_only(manifest):
+    """IAuxDetect eval (nets/iaux_detect.py:27-49): the plan's outputs are the
+    three main heads; the aux convs m2 and the layers feeding only them are
+    dead (their maps are discarded in eval) and never launched."""
+    e = manifest['g1']['iauxdetect']
+    m = Model(e['cfg'], ANCHORS, e['nc'])
+    assert len(m.state_dict()) == e['n_keys']  # same schema as the reference (m, m2, ia, im, anchors)
+    plan = Plan(m, tuple(e['shape']))
+    convs = [nd for nd in plan.graph.nodes if nd.kind in ('conv', 'stem')]
+    assert len(convs) == 4 + 3  # stem + 3 backbone convs + 3 main heads (aux layers 4-6 and m2 dropped)
+    assert [v.c for v in plan.out_vals] == [3 * (e['nc'] + 5)] * 3
+    assert [(v.h, v.w) for v in plan.out_vals] == [(12, 12), (6, 6), (3, 3)]

@@ -10,9 +10,10 @@ Reference API kept (same names, argument meaning, return types):
 
 Device tensors in, device kernels doing the work: decode_box runs ycx_decode
 per level; non_max_suppression runs ycx_filter_decoded (which also mutates
-``prediction[..., :4]`` to xyxy in place, like detect.py:98-103) and
-ycx_sort_nms, then copies the kept rows to the host for the numpy
-``yolo_correct_boxes`` step, exactly where the reference leaves the device.
+``prediction[..., :4]`` to xyxy in place, like detect.py:98-103),
+ycx_sort_nms and ycx_correct_boxes (the reference's numpy
+``yolo_correct_boxes`` step, reproduced bit for bit on the device); only the
+final per-image (K, 7) arrays are copied to the host.
 
 ``Detector`` is the fused fast path used by bench.py: forward -> fused
 decode+filter -> sort+NMS, all on device, static buffers, optional HIP graph.
@@ -146,25 +147,26 @@ def non_max_suppression(prediction, num_classes, input_shape, image_shape, lette
 
 
 def yolo_correct_boxes(box_xy, box_wh, input_shape, image_shape, letterbox_image):
-    """Undo the letterbox (numpy, host): returns [y1, x1, y2, x2] in pixels
-    (detect.py:147-165). The reference's host helper, kept for its callers;
-    non_max_suppression uses the device form (correct_boxes_device)."""
-    box_yx = box_xy[..., ::-1]
-    box_hw = box_wh[..., ::-1]
-    input_shape = np.array(input_shape)
-    image_shape = np.array(image_shape)
+    """Host form of the letterbox undo (detect.py:147-165), kept for the
+    reference's callers; non_max_suppression itself runs the device kernel
+    (correct_boxes_device). Returns [y1, x1, y2, x2] in original-image pixels.
+
+    Numerics follow the reference exactly: centres are corrected in float64,
+    sizes are scaled IN PLACE on the caller's float32 ``box_wh`` view (so they
+    stay float32 and the caller's array is modified, as in the reference), and
+    the final pixel scaling is an in-place multiply of the stacked corners."""
+    yx = box_xy[..., ::-1]
+    hw = box_wh[..., ::-1]
+    ins = np.array(input_shape)
+    img = np.array(image_shape)
     if letterbox_image:
-        new_shape = np.round(image_shape * np.min(input_shape / image_shape))
-        offset = (input_shape - new_shape) / 2. / input_shape
-        scale = input_shape / new_shape
-        box_yx = (box_yx - offset) * scale
-        box_hw *= scale
-    box_mins = box_yx - (box_hw / 2.)
-    box_maxes = box_yx + (box_hw / 2.)
-    boxes = np.concatenate([box_mins[..., 0:1], box_mins[..., 1:2], box_maxes[..., 0:1], box_maxes[..., 1:2]],
-                           axis=-1)
-    boxes *= np.concatenate([image_shape, image_shape], axis=-1)
-    return boxes
+        fitted = np.round(img * np.min(ins / img))
+        yx = (yx - (ins - fitted) / 2. / ins) * (ins / fitted)
+        hw *= ins / fitted
+    half = hw / 2.
+    corners = np.concatenate([yx - half, yx + half], axis=-1)
+    corners *= np.concatenate([img, img], axis=-1)
+    return corners
 
 
 def idetect_outputs(head, outs, input_hw):
@@ -261,9 +263,12 @@ class Detector:
     [sum na*H*W] candidates, -1 padded), keep_counts [n] (uncapped)."""
 
     def __init__(self, model, shape, device, anchors, anchors_mask, image_size=None, conf_thres=0.3,
-                 nms_thres=0.3, max_det=300, use_graph=True, slot=0):
+                 nms_thres=0.3, max_det=300, use_graph=True, slot=None):
         self.model = model
-        self.engine = model.engine_for(shape, device, slot)
+        # a private engine unless the caller names a slot: the static buffers of one
+        # Detector must never alias model(x)'s or another Detector's (in flight on
+        # another stream)
+        self.engine = model.engine_for(shape, device, model.new_slot() if slot is None else slot)
         self.device = torch.device(device)
         n, _, H, W = shape
         image_size = image_size or (H, W)
@@ -310,7 +315,7 @@ class PipelinedDetector:
 
     def __init__(self, model, shape, device, anchors, anchors_mask, depth=2, **kw):
         self.device = torch.device(device)
-        self.slots = [Detector(model, shape, device, anchors, anchors_mask, slot=k, **kw) for k in range(depth)]
+        self.slots = [Detector(model, shape, device, anchors, anchors_mask, **kw) for _ in range(depth)]
         # different priorities come from different stream pools and so land on
         # different hardware queues (two same-pool streams may share one)
         self.s_fwd = torch.cuda.Stream(self.device, priority=0)
@@ -332,6 +337,7 @@ class PipelinedDetector:
                 timing[0].record(self.s_fwd)
             if images is not None:
                 det.x.copy_(images)
+                images.record_stream(self.s_fwd)  # the caller may free it before this copy runs
             det.forward()
             self.fwd_done[k].record(self.s_fwd)
         with torch.cuda.stream(self.s_post):
@@ -363,7 +369,7 @@ class ConcurrentDetector:
 
     def __init__(self, model, shape, device, anchors, anchors_mask, depth=3, **kw):
         self.device = torch.device(device)
-        self.slots = [Detector(model, shape, device, anchors, anchors_mask, slot=k, **kw) for k in range(depth)]
+        self.slots = [Detector(model, shape, device, anchors, anchors_mask, **kw) for _ in range(depth)]
         # streams of our own, not torch pool streams: the pool is handed out
         # round-robin to every component (the RCCL communicator included), and a
         # slot stream that shares its hardware queue with the communicator's
@@ -390,6 +396,7 @@ class ConcurrentDetector:
                 timing[0].record(s)
             if images is not None:
                 det.x.copy_(images)
+                images.record_stream(s)  # the caller may free it before this copy runs
             det.forward()
             dets, keep, kc = det.post()
             if then is not None:

@@ -30,7 +30,7 @@ from torch import nn
 from . import _lib as L
 from .nets.common import (SP, SPP, SPPCSPC, SPPF, MP, Bottleneck, BottleneckCSPA, BottleneckCSPB, BottleneckCSPC,
                           Concat, Conv, RepConv)
-from .nets.detect import Detect, IDetect
+from .nets.detect import Detect, IAuxDetect, IDetect
 
 
 class Buf:
@@ -251,7 +251,7 @@ def lower_module(g: Graph, m, x):
             b = conv.bias.detach().to('cpu', torch.float64)
             outs.append(g.conv(x[idx], w, b, 1, 1, 0, head=True))
         return outs
-    if isinstance(m, IDetect):
+    if isinstance(m, IDetect):  # IAuxDetect too: its eval uses the main heads only (x[:nl])
         outs = []
         for i in range(m.nl):
             conv = m.m[i]
@@ -287,6 +287,7 @@ class Plan:
         self.is_list = isinstance(x, list)
         self.out_vals = list(x) if self.is_list else [x]
         self.graph = g
+        self._eliminate_dead()
         self._passes()
 
     @property
@@ -308,6 +309,21 @@ class Plan:
                 c['copy'] = c.get('copy', 0) + len(nd.p['copies'])
             c[kind] = c.get(kind, 0) + 1
         return c
+
+    def _eliminate_dead(self):
+        """Drop nodes whose value nobody reads (IAuxDetect's aux branch in eval:
+        nets/iaux_detect.py:32-33 computes it, :49 discards it)."""
+        g = self.graph
+        live = {id(v) for v in self.out_vals}
+        keep = []
+        for node in reversed(g.nodes):
+            if id(node.out) in live:
+                keep.append(node)
+                live.update(id(v) for v in node.inputs)
+            else:
+                for v in node.inputs:
+                    v.consumers = [c for c in v.consumers if c is not node]
+        g.nodes = keep[::-1]
 
     def _passes(self):
         g = self.graph
@@ -540,8 +556,8 @@ class Engine:
                 ops.append(self._conv_op(node))
             elif k == 'pool':
                 ops.append(self._pool_op(node))
-            elif k == 'up':
-                ops.append(self._copy_op(node.inputs[0], node.out, 0, scale=2))
+            elif k == 'up':  # an unfused upsample may write a slice of a concat buffer
+                ops.append(self._copy_op(node.inputs[0], node.out, node.out.coff, scale=2))
             elif k == 'concat':
                 for v, off in node.p['copies']:
                     ops.append(self._copy_op(v, node.out, off, scale=1))

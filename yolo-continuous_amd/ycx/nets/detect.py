@@ -7,6 +7,11 @@ IDetect — nets/idetect.py:7-50: ImplicitA -> 1x1 conv -> ImplicitM, reshaped t
           reference leaves ``stride`` as None so its eval raises TypeError
           (SURVEY.md Appendix B.7); here the strides default to
           image_size / ny per level (documented deviation).
+IAuxDetect — nets/iaux_detect.py:7-49: IDetect's main heads on x[:nl] plus
+          auxiliary 1x1 heads ``m2`` on x[nl:]. Eval returns
+          (cat(z, 1), x[:nl]): the aux maps are computed and discarded
+          (:32-33, :49), so the engine lowers only the main heads and the aux
+          branch is dead code it never launches.
 """
 from __future__ import annotations
 
@@ -52,3 +57,13 @@ class IDetect(_Holder):
         self.m = nn.ModuleList(nn.Conv2d(x, self.no * self.na, 1) for x in ch)
         self.ia = nn.ModuleList(ImplicitA(x) for x in ch)
         self.im = nn.ModuleList(ImplicitM(self.no * self.na) for _ in ch)
+
+
+class IAuxDetect(IDetect):
+    """Schema of nets/iaux_detect.py:11-25 (state_dict keys anchors, anchor_grid,
+    m.*, m2.*, ia.*, im.*). ``ch`` lists the main inputs then the aux inputs."""
+
+    def __init__(self, nc=80, anchors=(), ch=()):
+        nl = len(anchors)
+        super().__init__(nc, anchors, ch[:nl])
+        self.m2 = nn.ModuleList(nn.Conv2d(x, self.no * self.na, 1) for x in ch[nl:])

@@ -27,7 +27,7 @@ from torch import nn
 from ..utils.helper_io import cvt_cfg
 from .common import (SP, SPP, SPPCSPC, SPPF, MP, Bottleneck, BottleneckCSPA, BottleneckCSPB, BottleneckCSPC,
                      Concat, Conv, ImplicitA, ImplicitM, RepConv)
-from .detect import Detect, IDetect
+from .detect import Detect, IAuxDetect, IDetect
 
 
 def make_divisible(x, divisor):
@@ -38,7 +38,7 @@ _MODULES = {
     'Conv': Conv, 'MP': MP, 'SP': SP, 'Concat': Concat, 'SPPCSPC': SPPCSPC, 'RepConv': RepConv,
     'Bottleneck': Bottleneck, 'BottleneckCSPA': BottleneckCSPA, 'BottleneckCSPB': BottleneckCSPB,
     'BottleneckCSPC': BottleneckCSPC, 'SPP': SPP, 'SPPF': SPPF, 'ImplicitA': ImplicitA,
-    'ImplicitM': ImplicitM, 'Detect': Detect, 'IDetect': IDetect,
+    'ImplicitM': ImplicitM, 'Detect': Detect, 'IDetect': IDetect, 'IAuxDetect': IAuxDetect,
     'nn.Conv2d': nn.Conv2d, 'nn.BatchNorm2d': nn.BatchNorm2d, 'nn.Upsample': nn.Upsample,
 }
 # Reference modules constructible by its parse_model but used by neither shipped
@@ -46,7 +46,7 @@ _MODULES = {
 _OUT_OF_SCOPE = {
     'ReOrg', 'Chuncat', 'Shortcut', 'Foldcut', 'RobustConv', 'RobustConv2', 'GhostConv', 'Stem', 'DownC',
     'Res', 'ResX', 'Ghost', 'GhostSPPCSPC', 'GhostStem', 'dw_conv', 'Focus', 'Contract', 'Expand', 'Classify',
-    'TransformerLayer', 'TransformerBlock', 'IAuxDetect', 'IBin', 'RepBottleneck',
+    'TransformerLayer', 'TransformerBlock', 'IBin', 'RepBottleneck',
 } | {f'{p}{s}' for p in ('Res', 'ResX', 'RepRes', 'RepResX', 'Ghost', 'RepBottleneck')
      for s in ('CSPA', 'CSPB', 'CSPC')}
 
@@ -110,7 +110,7 @@ def parse_model(d, ch, anchors, num_classes):
             args = [ch[f]]
         elif m is Concat:
             c2 = sum(ch[x] for x in f)
-        elif m in (Detect, IDetect):
+        elif m in (Detect, IDetect, IAuxDetect):
             args.append([ch[x] for x in f])
             if isinstance(args[1], int):
                 args[1] = [list(range(args[1] * 2))] * len(f)
@@ -189,9 +189,9 @@ class Model(nn.Module):
         if self.training:
             raise RuntimeError("ycx: Model is inference-only on the HIP path (training is out of scope); "
                                "call .eval() first")
-        outs = self.engine_for(x.shape, x.device).run(x)
+        outs = self.engine_for(x.shape, x.device, slot=self.EAGER_SLOT).run(x)
         head = self.model[-1]
-        if isinstance(head, IDetect):  # eval branch: (z, x) as nets/idetect.py:45
+        if isinstance(head, IDetect):  # eval branch: (z, x[:nl]) as nets/idetect.py:45, nets/iaux_detect.py:49
             from ..detect import idetect_outputs
             return idetect_outputs(head, outs, x.shape[2:])
         return outs
@@ -214,9 +214,20 @@ class Model(nn.Module):
             self._fp8_amax = {}  # (H, W) -> calibration record
             self._prepacked = {}  # (precision, H, W) -> packed tensors (ycx.prepack)
 
+    EAGER_SLOT = -1  # the engine behind forward(): never shared with a Detector
+
+    def new_slot(self):
+        """A slot id no other caller holds: every Detector (and every slot of a
+        Pipelined/ConcurrentDetector) gets its own engine, i.e. its own
+        activation buffers, static input and heads, so work in flight on one
+        stream is never overwritten by another caller."""
+        self._slot_counter = getattr(self, '_slot_counter', 0) + 1
+        return 1000 + self._slot_counter
+
     def engine_for(self, shape, device, slot=0):
-        """The compiled plan for (shape, device, precision); ``slot`` > 0 gives an
-        independent copy (own activation buffers) for pipelined execution."""
+        """The compiled plan for (shape, device, precision); every distinct
+        ``slot`` is an independent copy (own activation buffers). ``forward``
+        uses ``EAGER_SLOT``; Detectors take fresh ids from ``new_slot``."""
         from ..engine import Engine
         shape = tuple(int(s) for s in shape)
         dev = torch.device(device)
