@@ -5,7 +5,7 @@
  * kernel, torchvision/csrc/ops/cpu/nms_kernel.cpp; torchvision is absent here
  * and unpinned, so this primitive is PARITY UNPINNED):
  *   areas = (x2 - x1) * (y2 - y1)                      fp32
- *   order = stable descending sort of the scores       ties keep input order
+ *   order = stable descending sort of the scores       ties keep input order, NaN last
  *   for i in order, unless suppressed: keep i; suppress every later j with
  *     (float)(w*h) / (float)(area_i + area_j - w*h) > iou_threshold   (fp32 ratio,
  *     compared in double), w = max(0, min(x2) - max(x1)), h likewise.
@@ -13,11 +13,24 @@
  * ref_post.nms; build with -ffp-contract=off (no FMA contraction) so the
  * roundings are identical. Used by the tests and bench.py's cpu_baseline leg
  * only, never by the product path. */
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
 static const float* g_scores;
+
+/* numpy's float32 maximum / minimum: a NaN operand propagates */
+static inline float np_max(float a, float b) { return (isnan(a) || a > b) ? a : b; }
+static inline float np_min(float a, float b) { return (isnan(a) || a < b) ? a : b; }
+
+/* argsort(-scores, kind='stable') order: key = -score ascending, NaN last */
+static inline int before(float sj, float si) {
+  const float kj = -sj, ki = -si;
+  if (isnan(kj)) return 0;
+  if (isnan(ki)) return 1;
+  return kj < ki;
+}
 
 static void merge_sort(int64_t* a, int64_t* tmp, int64_t n) {
   if (n < 2) return;
@@ -27,7 +40,7 @@ static void merge_sort(int64_t* a, int64_t* tmp, int64_t n) {
   int64_t i = 0, j = h, k = 0;
   while (i < h && j < n) {
     /* descending; on equal scores the earlier index first (stable) */
-    if (g_scores[a[j]] > g_scores[a[i]]) tmp[k++] = a[j++];
+    if (before(g_scores[a[j]], g_scores[a[i]])) tmp[k++] = a[j++];
     else tmp[k++] = a[i++];
   }
   while (i < h) tmp[k++] = a[i++];
@@ -64,13 +77,11 @@ int64_t ycx_oracle_nms(const float* boxes, const float* scores, int64_t n, doubl
       const int64_t j = order[c];
       if (sup[j]) continue;
       const float* bj = boxes + 4 * j;
-      const float xx1 = bi[0] > bj[0] ? bi[0] : bj[0];
-      const float yy1 = bi[1] > bj[1] ? bi[1] : bj[1];
-      const float xx2 = bi[2] < bj[2] ? bi[2] : bj[2];
-      const float yy2 = bi[3] < bj[3] ? bi[3] : bj[3];
-      float w = xx2 - xx1, h = yy2 - yy1;
-      w = 0.0f > w ? 0.0f : w;  /* np.maximum(0, .): NaN propagates like numpy */
-      h = 0.0f > h ? 0.0f : h;
+      const float xx1 = np_max(bi[0], bj[0]);
+      const float yy1 = np_max(bi[1], bj[1]);
+      const float xx2 = np_min(bi[2], bj[2]);
+      const float yy2 = np_min(bi[3], bj[3]);
+      const float w = np_max(0.0f, xx2 - xx1), h = np_max(0.0f, yy2 - yy1);
       const float inter = w * h;
       const float den = (areas[i] + areas[j]) - inter;
       const float ovr = inter / den;

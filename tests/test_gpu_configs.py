@@ -6,21 +6,25 @@ oracle (fp32 CPU restatement, pinned to the reference's goldens) recomputes the 
 and the last image only, which is what keeps this test to seconds on the host.
 
 Tolerances: bf16 forward 5e-2 of max |ref| per head (as tests/test_gpu_model.py);
-keep rows of the fused decode+NMS path: identical sets up to a handful of sigmoid-ulp
-boundary flips (as tests/test_gpu_post.py::test_detector_fused_path).
+the fused decode+NMS path is decomposed by helpers.fused_keep_report against the
+oracle chain on the same heads: decoded boxes <= 2e-6, membership flips only at
+conf_thres, keep rows bit-exact on the device's own candidates, and the
+end-to-end keep-set difference pinned to its measured value (KEEP_FLIPS_PIN).
 """
 import numpy as np
 import pytest
 import torch
 
-from helpers import ANCHORS, MASK, make_model, rel_err
-from oracle import ref_forward, ref_post
-from ycx.detect import Detector
+from helpers import ANCHORS, MASK, fused_keep_report, make_model, rel_err
+from oracle import ref_forward
+from ycx.detect import ConcurrentDetector, Detector
 from ycx.utils.helper_io import cvt_cfg
 from ycx.utils.synth import synthetic_images
 
 pytestmark = pytest.mark.gpu
 A = np.asarray(ANCHORS).reshape(-1, 2)
+C2_BAR, C5_BAR = 5e-2, 0.10   # heads: max |gpu - oracle| / max |oracle| (bf16, fp8 e4m3)
+KEEP_FLIPS_PIN = {'c2': 6, 'c5': 4, 'c4': 12}   # measured on MI355X: 3/0, 0/0, 6 (DESIGN.md §4)
 
 
 @pytest.fixture(scope='module')
@@ -34,7 +38,8 @@ def c4(device):
     torch.cuda.synchronize()
     heads = [h.cpu() for h in det.heads]
     ref = ref_forward.build(cvt_cfg('yolov7'), ANCHORS, 80, sd)(x[[0, 7]])
-    return dict(m=m, heads=heads, keep=keep.cpu(), kc=kc.cpu(), dets=dets.cpu(), ref=ref)
+    return dict(m=m, heads=heads, keep=keep.cpu(), kc=kc.cpu(), dets=dets.cpu(), ref=ref, cand=det.cand.cpu(),
+                cand_rows=det.cand_rows.cpu(), counts=det.counts.cpu())
 
 
 def test_c4_1280_forward_vs_oracle(c4):
@@ -45,15 +50,99 @@ def test_c4_1280_forward_vs_oracle(c4):
 
 
 def test_c4_1280_decode_nms_vs_oracle(c4):
-    heads0 = [h[:1] for h in c4['heads']]
-    dec = torch.cat(ref_post.decode_box(heads0, A, MASK, 80, (1280, 1280)), 1)
-    assert dec.shape == (1, 100800, 85)
-    ref_keep, _ = ref_post.nms_keep_rows(dec.clone(), 80, 0.3, 0.3)
-    k = int(c4['kc'][0])
-    assert k <= 50000 and k > 0
-    got = set(c4['keep'][0, :k].tolist())
-    want = set(ref_keep[0].tolist())
-    assert len(got ^ want) <= max(2, len(want) // 100), (len(got), len(want), len(got ^ want))
-    # every image of the batch produced detections and the padded tail is -1
-    assert all(int(c) > 0 for c in c4['kc'])
-    assert int(c4['keep'][0, k:].max()) == -1 if k < 50000 else True
+    assert all(int(c) > 0 for c in c4['kc'])  # every image of the batch produced detections
+    for b in (0,):
+        rep = fused_keep_report(c4['cand'], c4['cand_rows'], c4['counts'], c4['keep'], c4['kc'], b,
+                                [h[b] for h in c4['heads']], 80, 0.3, 0.3, 1280, 50000)
+        print(f"\nc4 image {b}: {rep}")
+        assert rep['cls_same'] and rep['nms_exact'], rep
+        assert rep['box_maxdiff'] <= 2e-6 and rep['member_max_dist'] <= 1e-6, rep
+        assert rep['keep_flips'] <= KEEP_FLIPS_PIN['c4'] and rep['unexplained_flips'] == 0, rep
+        k = int(c4['kc'][b])
+        assert 0 < k <= 50000 and (k == 50000 or int(c4['keep'][b, k:].max()) == -1)
+
+
+# ---------------------------------------------------------------------------
+# The benchmarked plans themselves (the conv tile picker depends on
+# M = n*Ho*Wo, so bs=2 tests do not run the kernels bench.py times). C2 and C5
+# are built exactly as bench.py builds them -- same Model, weights recipe,
+# ConcurrentDetector (3 slots on 3 HIP streams, HIP graphs), shape and
+# precision, hence the same conv descriptors and tiles -- with three batches in
+# flight; the last one is checked against the oracle.
+# ---------------------------------------------------------------------------
+
+
+def _bench_config(device, precision, bs, seed):
+    m, sd = make_model('yolov7', 80, 0, precision)
+    m.to(device)
+    shape = (bs, 3, 640, 640)
+    cd = ConcurrentDetector(m, shape, device, ANCHORS, MASK, depth=3, conf_thres=0.3, nms_thres=0.3, max_det=300)
+    x = synthetic_images(*shape, seed=seed)
+    for i in range(3):  # three batches in flight; the third (slot 2) is the one checked
+        cd.submit(x.to(device) if i == 2 else synthetic_images(*shape, seed=seed + 1 + i).to(device))
+    cd.synchronize()
+    torch.cuda.synchronize()
+    det = cd.slots[2]
+    tiles = {}
+    for info in det.engine.op_info:
+        tiles[info['name']] = tiles.get(info['name'], 0) + 1
+    print(f"\n{precision} bs={bs} plan tiles: {tiles}")
+    out = dict(heads=[h.cpu() for h in det.heads], cand=det.cand.cpu(), cand_rows=det.cand_rows.cpu(),
+               counts=det.counts.cpu(), keep=det.keep.cpu(), kc=det.kc.cpu(), tiles=tiles, bs=bs)
+    ref = ref_forward.build(cvt_cfg('yolov7'), ANCHORS, 80, sd)(x[[0, bs - 1]])
+    out['ref'] = ref
+    del cd, det
+    m.invalidate()
+    torch.cuda.empty_cache()
+    return out
+
+
+@pytest.fixture(scope='module')
+def c2(device):
+    return _bench_config(device, 'bf16', 32, 50)
+
+
+@pytest.fixture(scope='module')
+def c5(device):
+    return _bench_config(device, 'fp8', 64, 60)
+
+
+def _check_heads(cfg, bar):
+    bs = cfg['bs']
+    errs = []
+    for h, r in zip(cfg['heads'], cfg['ref']):
+        for gi, ri in ((0, 0), (bs - 1, 1)):
+            errs.append(rel_err(h[gi], r[ri]))
+    print(f"\nheads rel err (img 0, img {bs - 1}) per level: {[round(e, 4) for e in errs]}")
+    assert max(errs) < bar, errs
+
+
+def _check_keep(cfg, name):
+    for b in (0, cfg['bs'] - 1):
+        rep = fused_keep_report(cfg['cand'], cfg['cand_rows'], cfg['counts'], cfg['keep'], cfg['kc'], b,
+                                [h[b] for h in cfg['heads']], 80, 0.3, 0.3, 640, 300)
+        print(f"\n{name} image {b}: {rep}")
+        assert rep['cls_same'], "class ids differ on common candidates"
+        assert rep['box_maxdiff'] <= 2e-6, rep          # device decode vs oracle decode, normalised xyxy
+        assert rep['member_max_dist'] <= 1e-6, rep      # membership flips only at conf_thres
+        assert rep['nms_exact'], rep                    # keep rows bit-exact on the device's own candidates
+        assert rep['keep_flips'] <= KEEP_FLIPS_PIN[name] and rep['unexplained_flips'] == 0, rep
+
+
+def test_c2_bs32_bf16_forward_vs_oracle(c2):
+    assert [tuple(h.shape) for h in c2['heads']] == [(32, 255, 20, 20), (32, 255, 40, 40), (32, 255, 80, 80)]
+    _check_heads(c2, C2_BAR)
+
+
+def test_c2_bs32_bf16_keep_vs_oracle(c2):
+    _check_keep(c2, 'c2')
+
+
+def test_c5_bs64_fp8_forward_vs_oracle(c5):
+    assert [tuple(h.shape) for h in c5['heads']] == [(64, 255, 20, 20), (64, 255, 40, 40), (64, 255, 80, 80)]
+    assert any(k.startswith('f8_') for k in c5['tiles'])
+    _check_heads(c5, C5_BAR)
+
+
+def test_c5_bs64_fp8_keep_vs_oracle(c5):
+    _check_keep(c5, 'c5')

@@ -69,9 +69,17 @@ def test_g2_nets(device, manifest, g2, name, precision, tol):
         assert rel_err(o.cpu(), gold) < tol, (name, j, rel_err(o.cpu(), gold))
 
 
+DECODED_TOL = {'f32': 1e-3, 'bf16': 2e-2}   # decoded box / confidence tensors, max |gpu - ref| / max |ref|
+
+
 @pytest.mark.parametrize('precision,tol', [('f32', F32_TOL), ('bf16', BF16_TOL)])
 def test_yolov7_640_vs_oracle(device, precision, tol):
-    """Full BASELINE shape (640x640, COCO-80) at bs=2 against the oracle computed live."""
+    """Full BASELINE shape (640x640, COCO-80) at bs=2 against the oracle computed
+    live: the raw heads (Model.forward, nets/yolo.py:143-153) and the decoded
+    (N, 25200, 85) tensor (decode_box, detect.py:29-87) that north_star's
+    "1e-3 relative for box/confidence tensors" names -- boxes (cols 0-3),
+    objectness (col 4) and class confidences (cols 5-84) separately."""
+    from ycx.detect import decode_box
     m, sd = make_model('yolov7', 80, 0, precision)
     m.to(device)
     x = synthetic_images(2, 3, 640, 640, seed=3)
@@ -79,6 +87,15 @@ def test_yolov7_640_vs_oracle(device, precision, tol):
     outs = m(x.to(device))
     for o, r in zip(outs, ref):
         assert rel_err(o.cpu(), r) < tol
+    a = np.asarray(ANCHORS).reshape(-1, 2)
+    mask = [[6, 7, 8], [3, 4, 5], [0, 1, 2]]
+    dec = torch.cat(decode_box(outs, a, mask, 80, (640, 640)), 1).cpu()
+    dref = torch.cat(ref_post.decode_box(ref, a, mask, 80, (640, 640)), 1)
+    assert dec.shape == dref.shape == (2, 25200, 85)
+    errs = {k: rel_err(dec[..., sl], dref[..., sl]) for k, sl in
+            (('box', slice(0, 4)), ('obj', slice(4, 5)), ('cls', slice(5, 85)))}
+    print(f"\n{precision} decoded rel err: {errs}")
+    assert max(errs.values()) < DECODED_TOL[precision], errs
 
 
 def test_engine_plan_properties(device):

@@ -130,8 +130,15 @@ def test_oracle_c_nms_equals_numpy(seed):
     boxes[::97, 2:] = boxes[::97, :2]             # zero-area boxes
     boxes[1::53] = boxes[0::53][:boxes[1::53].shape[0]]  # exact duplicates
     scores = (torch.rand(n, generator=g) * 64).floor() / 64  # many exact ties
+    if seed == 2:  # non-finite inputs: numpy's NaN propagation and NaN-last argsort
+        boxes[5::211, 0] = float('nan')
+        boxes[7::307, 3] = float('inf')
+        boxes[11::401] = float('-inf')
+        scores[13::97] = float('nan')
+        scores[17::89] = float('inf')
     for thr in (0.3, 0.45, 0.7):
         a = nms(boxes, scores, thr)
-        b = nms_numpy(boxes, scores, thr)
+        with np.errstate(invalid='ignore'):
+            b = nms_numpy(boxes, scores, thr)
         assert torch.equal(a, b), (thr, len(a), len(b))
     assert len(nms(boxes[:0], scores[:0], 0.5)) == 0
