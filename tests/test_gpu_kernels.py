@@ -72,9 +72,7 @@ def _run_conv(device, n, h, w, cin, cout, k, s, act, tile, dtype, in_extra=0, ou
 
 TILES_BF16 = [(1, 128, 64), (2, 64, 64), (3, 64, 64), (4, 128, 64), (5, 32, 32), (6, 64, 32), (7, 128, 32),
               (9, 128, 64), (10, 64, 64), (11, 256, 128), (12, 128, 64), (13, 64, 32), (14, 128, 32), (14, 256, 32),
-              (15, 64, 64), (16, 128, 64), (17, 64, 32), (18, 64, 128),
-              (27, 256, 64), (27, 200, 128), (28, 128, 64), (28, 128, 192), (29, 256, 128),
-              (30, 256, 64), (31, 128, 192), (32, 128, 64), (33, 64, 64)]
+              (15, 64, 64), (16, 128, 64), (17, 64, 32), (18, 64, 128)]
 
 
 @pytest.mark.parametrize('tile,cout,cin', TILES_BF16)
@@ -83,6 +81,14 @@ def test_conv_bf16_tiles(device, tile, cout, cin, k, s):
     got, ref = _run_conv(device, 2, 13, 11, cin, cout, k, s, L.ACT_SILU, tile, L.DT_BF16, in_extra=8, out_extra=16)
     # bf16 output rounding (2^-8 relative) on top of exact products of bf16 inputs
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize('tile', [27, 31, 33])
+def test_retired_tiles_are_not_dispatched(device, tile):
+    """Tiles 27-33 (rejected experiments) exist only in a
+    -DYCX_EXPERIMENTAL_TILES build; the product library refuses them."""
+    with pytest.raises(L.YcxError, match='unsupported'):
+        _run_conv(device, 2, 13, 11, 64, 128, 3, 1, L.ACT_SILU, tile, L.DT_BF16)
 
 
 @pytest.mark.parametrize('tile,cin,cout', [(19, 64, 64), (19, 128, 192), (20, 64, 128), (20, 128, 256),

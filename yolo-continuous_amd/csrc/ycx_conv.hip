@@ -875,6 +875,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a) {
   else epilogue_f8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
 }
 
+#ifdef YCX_EXPERIMENTAL_TILES  // retired: measured 0.5-0.9x of the picked tiles
 // -------------------------------------------------------------------------
 // bf16 implicit-GEMM conv, ping-pong schedule (tiles 27-29). One 512-thread
 // block per CU, 8 waves as 2 (co) x 4 (px); a wave owns TM x TN outputs as four
@@ -1126,6 +1127,8 @@ __global__ void __launch_bounds__(512) conv_bf16_p8(ConvArgs a) {
 #pragma unroll
     for (int n = 0; n < 2; ++n) epilogue_regs<FM, FN>(a, acc[m][n], cob + m * QM, pxb + n * QN, lane);
 }
+
+#endif  // YCX_EXPERIMENTAL_TILES
 
 // -------------------------------------------------------------------------
 // 3x3 stride-1 conv from an LDS halo tile. A block owns a 16x16 output tile of
@@ -2354,13 +2357,13 @@ const TileInfo kTiles[] = {
     {256, 256, 64, "glds_co256_px256_k64_s2"},
     {256, 128, 64, "glds_co256_px128_k64_s2"},
     {128, 256, 64, "glds_co128_px256_k64_s2"},
-    {256, 256, 64, "p8_co256_px256"},
-    {128, 256, 64, "p8_co128_px256"},
-    {256, 128, 64, "p8_co256_px128"},
-    {256, 256, 64, "p8i_co256_px256"},
-    {128, 256, 64, "p8i_co128_px256"},
-    {128, 128, 64, "glds4w_co128_px128_k64_s2"},
-    {64, 128, 64, "glds4w_co64_px128_k64_s2"},
+    {256, 256, 64, "retired_p8_co256_px256"},     // 27-33: retired experiments, built only with
+    {128, 256, 64, "retired_p8_co128_px256"},     // -DYCX_EXPERIMENTAL_TILES
+    {256, 128, 64, "retired_p8_co256_px128"},
+    {256, 256, 64, "retired_p8i_co256_px256"},
+    {128, 256, 64, "retired_p8i_co128_px256"},
+    {128, 128, 64, "retired_glds4w_co128_px128"},
+    {64, 128, 64, "retired_glds4w_co64_px128"},
     {128, 128, 16, "f8_co128_px128_k128_s2"},
     {64, 128, 16, "f8_co64_px128_k128_s2"},
     {32, 64, 128, "f8_wres1x1"},
@@ -2439,6 +2442,7 @@ ycx_status launch_f8(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
+#ifdef YCX_EXPERIMENTAL_TILES
 template <int BM, int BN, bool DIM = false>
 ycx_status launch_p8(ConvArgs a, hipStream_t st) {
   if (a.Cin % 64 != 0 || a.Cout_pad % BM != 0) return YCX_ERR_UNSUPPORTED;
@@ -2448,6 +2452,7 @@ ycx_status launch_p8(ConvArgs a, hipStream_t st) {
   hipLaunchKernelGGL((conv_bf16_p8<BM, BN, DIM>), dim3(a.nwg), dim3(512), 0, st, a);
   return ycx_launch_status();
 }
+#endif
 
 // Weight-resident 1x1 (tile 22): the wave split follows cout_pad, the K unroll Cin.
 template <int WCO, int WPX, int TPW, int NS, int SUB>
@@ -2690,6 +2695,7 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
     case 24: return launch_glds<256, 256, 2, 4, false, 2>(a, st);
     case 25: return launch_glds<256, 128, 2, 4, false, 2>(a, st);
     case 26: return launch_glds<128, 256, 2, 4, false, 2>(a, st);
+#ifdef YCX_EXPERIMENTAL_TILES  // retired experiments (tools/build_variant.sh NAME -DYCX_EXPERIMENTAL_TILES)
     case 27: return launch_p8<256, 256>(a, st);
     case 28: return launch_p8<128, 256>(a, st);
     case 29: return launch_p8<256, 128>(a, st);
@@ -2697,6 +2703,7 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
     case 31: return launch_p8<128, 256, true>(a, st);
     case 32: return launch_glds<128, 128, 2, 2, false, 2>(a, st);
     case 33: return launch_glds<64, 128, 1, 4, false, 2>(a, st);
+#endif
     default: return YCX_ERR_UNSUPPORTED;
   }
 }
