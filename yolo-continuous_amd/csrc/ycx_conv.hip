@@ -426,6 +426,24 @@ __device__ __forceinline__ void buf_lds16(const void* base, int nbytes, int voff
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, soff, 0, 0);
 }
 
+#ifdef YCX_GLDS_STAMP
+// Development build only: per-phase cycle sums of the glds main loop. Each
+// stamp is an s_memtime whose result is consumed only at the end of the step
+// (one lgkmcnt(0) there, after the MFMAs already waited for the fragments).
+__device__ unsigned long long g_glds_stamp[8 * 8 + 1];
+__device__ __forceinline__ unsigned long long stamp_issue() {
+  unsigned long long v;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0" : "=s"(v));
+  __builtin_amdgcn_sched_barrier(0);
+  return v;
+}
+__device__ __forceinline__ void stamp_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+#define STAMP(k) unsigned long long st_t##k = stamp_issue()
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
 // TT (two taps per K step) serves Cin == 32: one 64-wide K step spans taps
 // 2s and 2s+1, and each lane's logical chunk c = pch ^ swz(row) (constant per
 // lane across steps) selects tap 2s + (c >> 2) and channels 8(c & 3). The
@@ -433,24 +451,33 @@ __device__ __forceinline__ void buf_lds16(const void* base, int nbytes, int voff
 // tap fetches zeros on the activation side (its weight chunk is finite).
 // NST = 2 halves the LDS so two workgroups share a CU: one block's prologue
 // and epilogue then overlap the other's MFMA loop (short-K layers).
-template <int BM, int BN, int WM, int WN, bool TT, int NST>
+template <int BM, int BN, int WM, int WN, bool TT, int NST, int NSB = NST>
 __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
   constexpr int NW = WM * WN;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(NST == 2 || NST == 3, "pipeline depth");
+  static_assert(NSB == NST || (NST == 2 && NSB == 3), "B ring: as deep as A's, or one deeper (2 / 3)");
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int A_PW = BM / (8 * NW), B_PW = BN / (8 * NW);  // wave-instructions (8 rows each) per wave per stage
   constexpr int LPS = A_PW + B_PW;                 // vmcnt per stage per wave
-  constexpr int LDS_BYTES = NST * STAGE;           // the epilogue stores straight from registers
+  // NSB == NST: NST stages of [A | B]. NSB > NST (split rings): the activation ring runs one
+  // K step further ahead than the weight ring (weights are L2-resident, activations come
+  // from HBM / the Infinity Cache): A ring [NST][A_BYTES] then B ring [NSB][B_BYTES].
+  constexpr bool SPLIT = NSB != NST;
+  constexpr int LDS_BYTES = SPLIT ? NST * A_BYTES + NSB * B_BYTES : NST * STAGE;
   static_assert(A_PW >= 1 && B_PW >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows per wave");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
   const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
   const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#ifdef YCX_GLDS_STAMP
+  unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long st_start = stamp_issue();
+#endif
   const int wm = wid / WN, wn = wid % WN;
   const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
   const int ct = L % a.n_ct, pt = L / a.n_ct;
@@ -493,10 +520,15 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
   int i_ky = 0, i_kx = 0, i_cb = 0;  // K position (first tap) of the next stage to issue
   const int ntaps = a.KH * a.KW;
   int i_tap = 0;
-  auto issue = [&](int s, int buf) {
-    char* base = smem + buf * STAGE;
+  auto a_slot = [&](int buf) { return SPLIT ? smem + buf * A_BYTES : smem + buf * STAGE; };
+  auto b_slot = [&](int buf) { return SPLIT ? smem + NST * A_BYTES + buf * B_BYTES : smem + buf * STAGE + A_BYTES; };
+  auto issueA = [&](int s, int buf) {
+    char* base = a_slot(buf);
 #pragma unroll
     for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * (BK * 2), base + (wid + NW * i) * 1024);
+  };
+  auto issueB = [&](int buf) {  // the next K step in (tap, channel) order
+    char* base = b_slot(buf);
     int ky = i_ky, kx = i_kx;
     if (TT) {
       // second tap of the pair; past the last tap it can never pass the bounds test
@@ -510,7 +542,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < B_PW; ++i) {
       const bool ok = (unsigned)(b_iy0[i] + ky) < (unsigned)a.H && (unsigned)(b_ix0[i] + kx) < (unsigned)a.W;
-      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + A_BYTES + (wid + NW * i) * 1024);
+      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + (wid + NW * i) * 1024);
     }
     if (TT) {
       i_tap += 2;
@@ -524,6 +556,10 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
       }
     }
   };
+  auto issue = [&](int s, int buf) {
+    issueA(s, buf);
+    issueB(buf);
+  };
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -532,16 +568,44 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nt = a.nsteps;
-  issue(0, 0);
-  if (NST == 3 && nt > 1) issue(1, 1);
+  if constexpr (SPLIT) {
+    // prologue A0, B0, B1; step t issues A(t+1) then B(t+2), so at the top of step t the
+    // wave's youngest outstanding DMA is B(t+1) (issued after A(t)): vmcnt(B_PW)
+    issueA(0, 0);
+    issueB(0);
+    if (nt > 1) issueB(1);
+  } else {
+    issue(0, 0);
+    if (NST == 3 && nt > 1) issue(1, 1);
+  }
+#ifdef YCX_GLDS_STAMP
+  unsigned long long st_prev = stamp_issue();
+  stamp_sync();
+  st_sum[0] = st_prev - st_start;
+#endif
   for (int t = 0; t < nt; ++t) {
-    if (NST == 3 && t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (SPLIT) {
+      if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_PW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (NST == 3 && t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    STAMP(1);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + NST - 1 < nt) issue(t + NST - 1, (t + NST - 1) % NST);
-    const __bf16* A = reinterpret_cast<const __bf16*>(smem + (t % NST) * STAGE);
-    const __bf16* B = reinterpret_cast<const __bf16*>(smem + (t % NST) * STAGE + A_BYTES);
+    STAMP(2);
+    if constexpr (SPLIT) {
+      if (t + 1 < nt) issueA(t + 1, (t + 1) % NST);
+      if (t + 2 < nt) issueB((t + 2) % NSB);
+    } else {
+      // DMA issued first thing after the barrier: issuing it after the fragment reads or
+      // between the MFMA halves measured 4-19 % slower (latency, not issue cost, binds)
+      if (t + NST - 1 < nt) issue(t + NST - 1, (t + NST - 1) % NST);
+    }
+    STAMP(3);
+    const __bf16* A = reinterpret_cast<const __bf16*>(a_slot(t % NST));
+    const __bf16* B = reinterpret_cast<const __bf16*>(b_slot(t % NSB));
     // all of the stage's fragments are requested before the first MFMA (left to
     // itself the compiler re-reads fragments between MFMAs to save registers,
     // exposing an LDS latency every two MFMAs)
@@ -561,6 +625,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
       }
     }
     __builtin_amdgcn_sched_barrier(0);
+    STAMP(4);
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk)
 #pragma unroll
@@ -569,14 +634,40 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
+    STAMP(5);
+#ifdef YCX_GLDS_STAMP
+    stamp_sync();
+    st_sum[1] += st_t1 - st_prev;
+    st_sum[2] += st_t2 - st_t1;
+    st_sum[3] += st_t3 - st_t2;
+    st_sum[4] += st_t4 - st_t3;
+    st_sum[5] += st_t5 - st_t4;
+    st_prev = st_t5;
+#endif
   }
+  bool done = false;
   if constexpr (FM % 2 == 0) {
     if (perm) {
       epilogue_regs8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
-      return;
+      done = true;
     }
   }
-  epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+  if (!done) epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+#ifdef YCX_GLDS_STAMP
+  {
+    const unsigned long long e = stamp_issue();
+    stamp_sync();
+    st_sum[6] = e - st_prev;
+    st_sum[7] = e - st_start;
+  }
+  if (lane < 8) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v = lane == b ? st_sum[b] : v;
+    atomicAdd(&g_glds_stamp[(wid & 7) * 8 + lane], v);
+  }
+  if (tid == 0) atomicAdd(&g_glds_stamp[64], 1ull);
+#endif
 }
 
 // -------------------------------------------------------------------------
@@ -809,7 +900,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a) {
     for (int i = 0; i < B_PW; ++i) {
       const bool ok = tap_ok && (unsigned)(b_iy0[i] + ky) < (unsigned)a.H &&
                       (unsigned)(b_ix0[i] + kx) < (unsigned)a.W;
-      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + A_BYTES + (wid + NW * i) * 1024);
+      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + (wid + NW * i) * 1024);
     }
     if (TPS == 1) {
       cb += RB;
@@ -2411,14 +2502,14 @@ ycx_status launch_halo(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
-template <int BM, int BN, int WM, int WN, bool TT = false, int NST = 3>
+template <int BM, int BN, int WM, int WN, bool TT = false, int NST = 3, int NSB = NST>
 ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   if (TT && a.Cin != 32) return YCX_ERR_UNSUPPORTED;
   if (!TT && a.Cin % 64 != 0) return YCX_ERR_UNSUPPORTED;
   a.nsteps = TT ? (a.KH * a.KW + 1) / 2 : a.KH * a.KW * (a.Cin / 64);
   a.n_ct = a.Cout_pad / BM;
   a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
+  hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST, NSB>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
   return ycx_launch_status();
 }
 
@@ -2818,3 +2909,14 @@ extern "C" ycx_status ycx_stem_conv2(const ycx_conv_desc* sd, const ycx_conv_des
 #undef YCX_STEM2
   return YCX_ERR_UNSUPPORTED;
 }
+
+#ifdef YCX_GLDS_STAMP
+extern "C" int ycx_debug_glds_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_glds_stamp), sizeof(g_glds_stamp)) != hipSuccess) return 1;
+  if (reset) {
+    unsigned long long z[8 * 8 + 1] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_glds_stamp), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
