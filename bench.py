@@ -69,6 +69,8 @@ def parse(argv=None):
                     help="fixed-load decode + NMS micro-bench on G3-recipe head logits (SURVEY 8(d)) instead of "
                          "the network bench; prints its own JSON line")
     ap.add_argument("--obj-shift", type=float, default=-3.0, help="--post-micro: objectness logit shift")
+    ap.add_argument("--diag-forward-only", action="store_true",
+                    help="DIAGNOSTIC (not the metric): time the forwards alone, no decode / NMS")
     return ap.parse_args(argv)
 
 
@@ -346,7 +348,8 @@ def main():
     def step(i=None):
         timing = lat_ev[i] if i is not None else None
         if mode == "concurrent":  # the collective on the batch's own stream, issued in batch order on every rank
-            dets, keep, kc, done = det.submit(timing=timing, then=gather if dist_on else None)
+            dets, keep, kc, done = det.submit(timing=timing, then=gather if dist_on else None,
+                                              post=not args.diag_forward_only)
             return kc
         if pipeline:
             dets, keep, kc, _ = det.submit(timing=timing)

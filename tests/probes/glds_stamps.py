@@ -26,7 +26,7 @@ def main():
     lib.ycx_debug_glds_stamps.restype = ctypes.c_int
     lib.ycx_debug_glds_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     dev = torch.device("cuda:0")
-    buf = (ctypes.c_ulonglong * 65)()
+    buf = (ctypes.c_ulonglong * 129)()
     for i in idx:
         n, h, w, cin, cout, k, s = SHAPES[i]
         p = k // 2
@@ -53,11 +53,11 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         lib.ycx_debug_glds_stamps(buf, 1)
-        wgs = buf[64]
+        wgs = buf[128]
         print(f"{SHAPES[i]} tile {tile}: {e0.elapsed_time(e1) / 10 * 1e3:.1f} us/launch, {wgs // 10} WGs/launch")
         for wv in (0, 4):
             row = [buf[wv * 8 + b] / wgs for b in range(8)]
-            print(f"  wave {wv}: " + "  ".join(f"{nm} {v:8.0f}" for nm, v in zip(NAMES, row)))
+            print(f"  wave {wv}: " + "  ".join(f"{n} {v:8.0f}" for n, v in zip(NAMES, row)))
         print(flush=True)
 
 

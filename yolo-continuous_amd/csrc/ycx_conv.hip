@@ -430,7 +430,7 @@ __device__ __forceinline__ void buf_lds16(const void* base, int nbytes, int voff
 // Development build only: per-phase cycle sums of the glds main loop. Each
 // stamp is an s_memtime whose result is consumed only at the end of the step
 // (one lgkmcnt(0) there, after the MFMAs already waited for the fragments).
-__device__ unsigned long long g_glds_stamp[8 * 8 + 1];
+__device__ unsigned long long g_glds_stamp[16 * 8 + 1];
 __device__ __forceinline__ unsigned long long stamp_issue() {
   unsigned long long v;
   __builtin_amdgcn_sched_barrier(0);
@@ -664,9 +664,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
     unsigned long long v = 0;
 #pragma unroll
     for (int b = 0; b < 8; ++b) v = lane == b ? st_sum[b] : v;
-    atomicAdd(&g_glds_stamp[(wid & 7) * 8 + lane], v);
+    atomicAdd(&g_glds_stamp[(wid & 15) * 8 + lane], v);
   }
-  if (tid == 0) atomicAdd(&g_glds_stamp[64], 1ull);
+  if (tid == 0) atomicAdd(&g_glds_stamp[128], 1ull);
 #endif
 }
 
@@ -2914,7 +2914,7 @@ extern "C" ycx_status ycx_stem_conv2(const ycx_conv_desc* sd, const ycx_conv_des
 extern "C" int ycx_debug_glds_stamps(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_glds_stamp), sizeof(g_glds_stamp)) != hipSuccess) return 1;
   if (reset) {
-    unsigned long long z[8 * 8 + 1] = {};
+    unsigned long long z[16 * 8 + 1] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_glds_stamp), z, sizeof(z)) != hipSuccess) return 1;
   }
   return 0;

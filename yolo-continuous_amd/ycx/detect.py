@@ -383,10 +383,11 @@ class ConcurrentDetector:
     def s_post(self):  # the stream of the most recent batch (where its collective goes)
         return self.streams[(self.i - 1) % len(self.slots)]
 
-    def submit(self, images=None, timing=None, then=None):
+    def submit(self, images=None, timing=None, then=None, post=True):
         """Enqueue one batch on the next slot's stream. ``then(dets, keep, kc)``,
         if given, runs on that stream right after the NMS (the multi-GPU path
-        issues its all-gather there) and its return value replaces the outputs."""
+        issues its all-gather there) and its return value replaces the outputs.
+        ``post=False`` (diagnostics only) enqueues the forward alone."""
         k = self.i % len(self.slots)
         self.i += 1
         det, s = self.slots[k], self.streams[k]
@@ -398,7 +399,7 @@ class ConcurrentDetector:
                 det.x.copy_(images)
                 images.record_stream(s)  # the caller may free it before this copy runs
             det.forward()
-            dets, keep, kc = det.post()
+            dets, keep, kc = det.post() if post else (det.dets, det.keep, det.kc)
             if then is not None:
                 dets, keep, kc = then(dets, keep, kc)
             self.done[k].record(s)
