@@ -276,15 +276,3 @@ def test_stem_conv2_fused(device, stem_s, cout, act):
     got = t[5].cpu()
     assert torch.all(got[..., :out_extra] == 0)
     torch.testing.assert_close(got[..., out_extra:].permute(0, 3, 1, 2).double(), ref, rtol=2e-2, atol=2e-2)
-
-
-@pytest.mark.parametrize('tile', [27, 28, 29, 30, 31])
-@pytest.mark.parametrize('layout,residual', [(L.OUT_NHWC, False), (L.OUT_NHWC, True), (L.OUT_NHWC_UP2, False),
-                                             (L.OUT_NCHW_F32, False)])
-def test_conv_p8_many_ktiles(device, tile, layout, residual):
-    """Ping-pong 8-phase tiles: 36 K tiles (the steady-state DMA ring and its
-    tail), several pixel and channel tiles, ragged pixel tail, all epilogues."""
-    cout = 255 if layout == L.OUT_NCHW_F32 else 256
-    got, ref = _run_conv(device, 2, 19, 21, 256, cout, 3, 1, L.ACT_SILU, tile, L.DT_BF16, in_extra=0,
-                         out_extra=0 if layout == L.OUT_NCHW_F32 else 8, residual=residual, layout=layout)
-    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)

@@ -900,7 +900,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a) {
     for (int i = 0; i < B_PW; ++i) {
       const bool ok = tap_ok && (unsigned)(b_iy0[i] + ky) < (unsigned)a.H &&
                       (unsigned)(b_ix0[i] + kx) < (unsigned)a.W;
-      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + (wid + NW * i) * 1024);
+      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + A_BYTES + (wid + NW * i) * 1024);
     }
     if (TPS == 1) {
       cb += RB;

@@ -558,9 +558,10 @@ __device__ void resolve(const Ctx<kLds>& c, const Frame& fr, const Ptrs& P, unsi
     const f32x4 b = c.sbox[p];
     const float a = box_area(b);
     const Geo g = geometry(b, fr.X0, fr.Y0, fr.inv, fr.all_pairs);
-    int top[kSlots];
-#pragma unroll
-    for (int k = 0; k < kSlots; ++k) top[k] = 0x7FFFFFFF;
+    // the box's kSlots highest-ranked suppressors (unordered: appended while the
+    // list has room, then the lowest-ranked replaced) and their total count; a box
+    // needs a rescan only when the cached ones all end up removed while more exist
+    int* sl = P.slots + (size_t)(off + p) * kSlots;
     int ns = 0;
 #ifdef YCX_NMS_PROFILE
     int visits = 0;
@@ -569,12 +570,15 @@ __device__ void resolve(const Ctx<kLds>& c, const Frame& fr, const Ptrs& P, unsi
       // for thr >= 0 a suppressor must overlap (inter > 0): four compares first
       const bool cand = rj < r && (fr.all_pairs || (o[0] < b[2] && o[2] > b[0] && o[1] < b[3] && o[3] > b[1]));
       if (cand && suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
-        int v = rj;
-#pragma unroll
-        for (int k = 0; k < kSlots; ++k) {
-          const int lo = min(v, top[k]);
-          v = max(v, top[k]);
-          top[k] = lo;
+        if (ns < kSlots) {
+          sl[ns] = rj;
+        } else {  // rare (a few % of the boxes): keep the kSlots highest-ranked (smallest ranks)
+          int km = 0, vm = sl[0];
+          for (int k = 1; k < kSlots; ++k) {
+            const int v = sl[k];
+            if (v > vm) { vm = v; km = k; }
+          }
+          if (rj < vm) sl[km] = rj;
         }
         ++ns;
       }
@@ -598,10 +602,6 @@ __device__ void resolve(const Ctx<kLds>& c, const Frame& fr, const Ptrs& P, unsi
       for (; q < q1; ++q) test(c.rank(q), c.sbox[q]);
       return true;
     });
-    int* sl = P.slots + (size_t)(off + p) * kSlots;
-#pragma unroll
-    for (int k = 0; k < kSlots; ++k)
-      if (k < ns) sl[k] = top[k];
     P.nsup[off + p] = ns;
 #ifdef YCX_NMS_PROFILE
     if (ns > kSlots) atomicAdd(&g_nms_prof[6], 1ull);
