@@ -33,7 +33,7 @@ ANCHORS = [[12, 16, 19, 36, 40, 28], [36, 75, 76, 55, 72, 146], [142, 110, 192, 
 MASK = [[6, 7, 8], [3, 4, 5], [0, 1, 2]]
 METRIC = "images/sec (whole node) + p50 end-to-end latency, 640×640 bs=32, 1/2/4/8 MI355X"
 PEAK = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
-ROUND = "r01"  # profiles/<ROUND>/: rocprofv3 summaries of this round's bench command
+ROUND = "r02"  # profiles/<ROUND>/: rocprofv3 summaries of this round's bench command
 
 
 def parse(argv=None):
@@ -60,6 +60,10 @@ def parse(argv=None):
                     help="0: skip the CPU baseline; --post-micro: time budget of its CPU leg")
     ap.add_argument("--cpu-batch", type=int, default=32, help="CPU baseline batch (BASELINE.md §4: 32)")
     ap.add_argument("--cpu-iters", type=int, default=3, help="CPU baseline timed iterations (after 1 warm-up)")
+    ap.add_argument("--no-fuse-heads", action="store_true",
+                    help="diagnostic: decode in a separate ycx_decode_filter pass over stored fp32 heads")
+    ap.add_argument("--keep-heads", action="store_true",
+                    help="diagnostic: the fused head convs also store the raw fp32 NCHW logits")
     ap.add_argument("--roofline-steps", type=int, default=3)
     ap.add_argument("--dist", action="store_true",
                     help="run the N > 1 code path (process group + RCCL all-gather) even at one rank")
@@ -201,7 +205,8 @@ def setup(args, dev, rank=0, use_graph=None, pipeline=False):
     model.to(dev)
     shape = (args.batch, 3, args.size, args.size)
     kw = dict(conf_thres=args.conf, nms_thres=args.iou, max_det=args.max_det,
-              use_graph=(not args.no_graph) if use_graph is None else use_graph)
+              use_graph=(not args.no_graph) if use_graph is None else use_graph,
+              fuse_heads=not getattr(args, 'no_fuse_heads', False), keep_heads=getattr(args, 'keep_heads', False))
     images = synthetic_images(*shape, seed=1000 + rank).to(dev)
     if pipeline:
         if pipeline == 'pipelined':

@@ -23,6 +23,8 @@
  *   ycx_decode          decode_box (one head level)             detect.py:29-87
  *   ycx_filter_decoded  non_max_suppression lines 98-121        detect.py:98-121
  *   ycx_decode_filter   decode_box + the same filter, fused     detect.py:29-121
+ *   ycx_conv2d_head     Detect head conv (one level) fused with  nets/detect.py:27-38 +
+ *                       decode_box + the candidate filter        detect.py:29-121
  *   ycx_idetect_decode  IDetect eval branch (strides supplied)  nets/idetect.py:33-45
  *   ycx_sort_nms        per-class torchvision.ops.nms loop      detect.py:124-137
  *   ycx_run_ops         Model.forward layer loop                nets/yolo.py:143-153
@@ -40,7 +42,7 @@
 extern "C" {
 #endif
 
-#define YCX_ABI_VERSION 3
+#define YCX_ABI_VERSION 4
 
 typedef int32_t ycx_status;
 enum {
@@ -175,8 +177,19 @@ typedef struct ycx_correct_desc {
   int32_t letterbox;          /* letterbox_image flag                      */
 } ycx_correct_desc;
 
+/* Decode + candidate filter of one Detect head level, fused into the head's
+ * 1x1 conv (ycx_conv2d_head): the fp32 logits of a tile never leave the CU.
+ * Candidates are the same as ycx_decode_filter's for this level (same float
+ * operations in the same order): rows row_off + a * h * w + cell. */
+typedef struct ycx_head_desc {
+  int32_t na, no, nc;           /* anchors, outputs per anchor (nc + 5), classes      */
+  int32_t rows_total, row_off;  /* candidate rows per image (all levels), this level's */
+  float conf_thres;             /* obj * cls_conf >= conf_thres, compared in fp32     */
+  float anchors_scaled[16];     /* as ycx_decode_desc                                 */
+} ycx_head_desc;
+
 /* A pre-built op for ycx_run_ops (the static execution plan of Model.forward). */
-enum { YCX_OP_CONV = 1, YCX_OP_STEM = 2, YCX_OP_POOL = 3, YCX_OP_COPY = 4, YCX_OP_STEM2 = 5 };
+enum { YCX_OP_CONV = 1, YCX_OP_STEM = 2, YCX_OP_POOL = 3, YCX_OP_COPY = 4, YCX_OP_STEM2 = 5, YCX_OP_HEAD = 6 };
 typedef struct ycx_op {
   int32_t kind;
   int32_t pad_;
@@ -185,6 +198,10 @@ typedef struct ycx_op {
     ycx_pool_desc pool;
     ycx_copy_desc copy;
     ycx_conv_desc pair[2];  /* STEM2: [0] the stem, [1] the stride-2 conv it feeds */
+    struct {
+      ycx_conv_desc conv;
+      ycx_head_desc head;
+    } head;                 /* HEAD: the head conv and its level's decode           */
   } d;
   const void* in;           /* x                                                    */
   const void* weight;       /* packed weights (conv/stem; STEM2: the stem's)        */
@@ -193,12 +210,16 @@ typedef struct ycx_op {
   const void* residual;     /* optional residual (conv)                             */
   const void* weight2;      /* STEM2: the second conv's packed bf16 weights         */
   const float* bias2;       /* STEM2: the second conv's bias                        */
+  void* cand;               /* HEAD: ycx_cand [n][rows_total]                      */
+  int32_t* cand_rows;       /* HEAD: [n][rows_total]                                */
+  int32_t* cand_counts;     /* HEAD: [n], zeroed before the first level's op        */
 } ycx_op;
 
 int ycx_abi_version(void);
 /* sizeof() of the ABI structs, so FFI mirrors can verify their layout:
  * 0 conv_desc, 1 pool_desc, 2 copy_desc, 3 decode_desc, 4 cand, 5 filter_desc,
- * 6 decode_filter_desc, 7 nms_desc, 8 op, 9 letterbox_desc, 10 correct_desc.
+ * 6 decode_filter_desc, 7 nms_desc, 8 op, 9 letterbox_desc, 10 correct_desc,
+ * 11 head_desc.
  * Returns 0 for an unknown id. */
 size_t ycx_struct_size(int32_t which);
 const char* ycx_strerror(ycx_status s);
@@ -209,6 +230,14 @@ int32_t ycx_conv_pick_tile(const ycx_conv_desc* d);
 
 ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const void* w,
                       const float* bias, void* y, const void* residual, void* stream);
+/* Detect head 1x1 conv of one level (bf16, act none, cout = na * no <= 256,
+ * out_layout YCX_OUT_NCHW_F32) fused with that level's decode + filter: appends
+ * the passing rows to cand / cand_rows / cand_counts exactly as
+ * ycx_decode_filter does. `heads` (nullable) also receives the raw fp32 NCHW
+ * logits [n][cout][ho][wo] (the compat Model.forward output). */
+ycx_status ycx_conv2d_head(const ycx_conv_desc* d, const ycx_head_desc* h, const void* x, const void* w,
+                           const float* bias, float* heads, ycx_cand* cand, int32_t* cand_rows,
+                           int32_t* cand_counts, void* stream);
 /* Stem conv: fp32 NCHW input (the model input, cin <= 4), weights fp32
  * [kh][kw][cin][cout_pad], output NHWC in d->dtype. in_c_* describe the NCHW
  * channel count (in_c_stride = channels of the input tensor). */

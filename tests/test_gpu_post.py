@@ -186,6 +186,47 @@ def test_nms_edge_cases(device):
         np.testing.assert_array_equal(keep[0, :k].cpu().numpy(), ref_keep[0].numpy())
 
 
+def _sorted_cands(det, b):
+    n = int(det.counts[b])
+    rows = torch.sort(det.cand_rows[b, :n].cpu()).values
+    return rows, det.cand[b].cpu()[rows.long()]   # ycx_cand is indexed by row, cand_rows lists the rows
+
+
+@pytest.mark.parametrize('cfg,nc,shape', [('yolov7-tiny', 1, (3, 3, 224, 224)), ('yolov7-tiny', 80, (2, 3, 320, 256)),
+                                          ('yolov7', 80, (2, 3, 256, 256))])
+def test_head_decode_fused_in_conv(device, cfg, nc, shape):
+    """ycx_conv2d_head (decode + filter in the Detect-head conv epilogue) vs the
+    unfused chain (head conv -> fp32 NCHW heads -> ycx_decode_filter) on the
+    same model and images: raw heads, candidate rows and values, keep rows and
+    dets are all bit-identical, with and without the raw-head store. 224 and
+    320x256 put 64-pixel head tiles across image boundaries (7x7, 10x8 grids)."""
+    m, _ = make_model(cfg, nc, 0, 'bf16')
+    m.to(device)
+    x = synthetic_images(*shape, seed=31).to(device)
+    conf = 0.3 if nc == 1 else 0.05   # random-init nc=80 scores are ~0.5*0.5; keep the filter busy
+    kw = dict(conf_thres=conf, nms_thres=0.45, max_det=1000)
+    ref = Detector(m, shape, device, ANCHORS, MASK, fuse_heads=False, **kw)
+    fz = Detector(m, shape, device, ANCHORS, MASK, keep_heads=True, **kw)
+    fn = Detector(m, shape, device, ANCHORS, MASK, keep_heads=False, **kw)
+    assert not ref.fused and fz.fused and fn.fused
+    assert sum(i['kind'] == 'head' for i in fz.engine.op_info) == 3
+    want = [t.clone() for t in ref(x)]
+    for det in (fz, fn):
+        for rep in range(2):   # replays reset the counts
+            got = [t.clone() for t in det(x)]
+            torch.cuda.synchronize()
+            assert torch.equal(det.counts, ref.counts)
+            for b in range(shape[0]):
+                r1, c1 = _sorted_cands(ref, b)
+                r2, c2 = _sorted_cands(det, b)
+                assert torch.equal(r1, r2) and torch.equal(c1, c2)
+            for w, g in zip(want, got):
+                assert torch.equal(w, g)
+    for h1, h2 in zip(ref.heads, fz.heads):
+        assert torch.equal(h1, h2)
+    assert int(ref.counts.sum()) > 0
+
+
 @pytest.mark.parametrize('precision', ['f32', 'bf16'])
 def test_detector_fused_path(device, precision):
     """Fused decode+filter+sort+NMS from the model's own heads vs the oracle

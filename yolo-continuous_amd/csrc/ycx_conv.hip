@@ -444,6 +444,93 @@ __device__ __forceinline__ void stamp_sync() { asm volatile("s_waitcnt lgkmcnt(0
 #define STAMP(k) do { } while (0)
 #endif
 
+// Fused Detect-head epilogue (tile 38, ycx_conv2d_head): the workgroup holds
+// all na * no channels of BN pixels; the biased fp32 logits go through LDS and
+// one thread per (pixel, anchor) applies decode_box + the candidate filter of
+// detect.py:29-121 with the float operations of ycx_post.hip's
+// decode_filter_kernel, in the same order (FMA contraction off here too), so
+// the candidates are bit-identical to the unfused path. Optional raw fp32 NCHW
+// stores (the compat Model.forward output) are coalesced along pixels.
+struct HeadArgs {
+  ycx_head_desc h;
+  ycx_cand* cand;
+  int* rows_out;
+  int* counts;
+  float* heads;
+};
+
+__device__ __forceinline__ float head_sigmoid(float v) {
+#pragma clang fp contract(off)
+  return 1.0f / (1.0f + expf(-v));
+}
+
+template <int BN>
+__device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const float* T, int ldt, int px0) {
+#pragma clang fp contract(off)
+  const ycx_head_desc& h = hd.h;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int HW = a.HoWo, W = a.Wo, H = a.Ho;
+  if (hd.heads) {  // raw logits, fp32 NCHW: 64 consecutive pixels of one channel per wave-instruction
+    for (int e = tid; e < a.Cout * BN; e += blockDim.x) {
+      const int c = e / BN, px = e - c * BN, p = px0 + px;
+      if (p < a.M) {
+        const int n = p / HW, cell = p - n * HW;
+        hd.heads[((size_t)n * a.Cout + c) * HW + cell] = T[c * ldt + px];
+      }
+    }
+  }
+  for (int it = tid; it < ((h.na * BN + 63) & ~63); it += blockDim.x) {  // whole waves: appends are wave-wide
+    const int an = it / BN, px = it - an * BN, p = px0 + px;
+    const bool valid = an < h.na && p < a.M;
+    const int n = valid ? p / HW : 0, cell = valid ? p - n * HW : 0;
+    bool pass = false;
+    ycx_cand c;
+    if (valid) {
+      const float* L = T + (size_t)(an * h.no) * ldt + px;
+      const float obj = head_sigmoid(L[4 * ldt]);
+      if (obj >= h.conf_thres) {  // obj * cls <= obj: otherwise the row cannot pass
+        float best = head_sigmoid(L[5 * ldt]);
+        int bi = 0;
+        for (int k = 1; k < h.nc; ++k) {
+          const float sv = head_sigmoid(L[(5 + k) * ldt]);
+          if (sv > best) { best = sv; bi = k; }
+        }
+        const float score = obj * best;
+        if (score >= h.conf_thres) {
+          const float gx = (float)(cell % W), gy = (float)(cell / W);
+          const float px_ = head_sigmoid(L[0]), py = head_sigmoid(L[ldt]);
+          const float pw = head_sigmoid(L[2 * ldt]), ph = head_sigmoid(L[3 * ldt]);
+          const float bx = ((px_ * 2.0f) - 0.5f + gx) / (float)W;
+          const float by = ((py * 2.0f) - 0.5f + gy) / (float)H;
+          const float tw = pw * 2.0f, th = ph * 2.0f;
+          const float bw = (tw * tw * h.anchors_scaled[2 * an]) / (float)W;
+          const float bhh = (th * th * h.anchors_scaled[2 * an + 1]) / (float)H;
+          pass = true;
+          c = ycx_cand{bx - bw / 2.0f, by - bhh / 2.0f, bx + bw / 2.0f, by + bhh / 2.0f, obj, best, bi,
+                       h.row_off + an * HW + cell};
+        }
+      }
+    }
+    // wave-aggregated append per image (a tile spans at most a few images)
+    unsigned long long rem = __ballot(pass);
+    while (rem) {
+      const int leader = __ffsll((long long)rem) - 1;
+      const int nl = __shfl(n, leader);
+      const bool mine = pass && n == nl;
+      const unsigned long long m = __ballot(mine);
+      int base = 0;
+      if (lane == leader) base = atomicAdd(hd.counts + nl, __popcll(m));
+      base = __shfl(base, leader);
+      if (mine) {
+        const int slot = base + __popcll(m & ((1ull << lane) - 1ull));
+        hd.cand[(size_t)nl * h.rows_total + c.row] = c;
+        hd.rows_out[(size_t)nl * h.rows_total + slot] = c.row;
+      }
+      rem &= ~m;
+    }
+  }
+}
+
 // TT (two taps per K step) serves Cin == 32: one 64-wide K step spans taps
 // 2s and 2s+1, and each lane's logical chunk c = pch ^ swz(row) (constant per
 // lane across steps) selects tap 2s + (c >> 2) and channels 8(c & 3). The
@@ -451,8 +538,8 @@ __device__ __forceinline__ void stamp_sync() { asm volatile("s_waitcnt lgkmcnt(0
 // tap fetches zeros on the activation side (its weight chunk is finite).
 // NST = 2 halves the LDS so two workgroups share a CU: one block's prologue
 // and epilogue then overlap the other's MFMA loop (short-K layers).
-template <int BM, int BN, int WM, int WN, bool TT, int NST, int NSB = NST>
-__global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
+template <int BM, int BN, int WM, int WN, bool TT, int NST, int NSB = NST, bool HEAD = false>
+__global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadArgs hd) {
   constexpr int NW = WM * WN;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(NST == 2 || NST == 3, "pipeline depth");
@@ -469,6 +556,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
   constexpr bool SPLIT = NSB != NST;
   constexpr int LDS_BYTES = SPLIT ? NST * A_BYTES + NSB * B_BYTES : NST * STAGE;
   static_assert(A_PW >= 1 && B_PW >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows per wave");
+  constexpr int HEAD_LDT = BN + 1;  // HEAD: fp32 logits [BM][BN + 1] (odd stride: conflict-free writes)
+  static_assert(!HEAD || BM * HEAD_LDT * 4 <= LDS_BYTES, "head tile fits the stages");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
   const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
@@ -646,13 +735,32 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a) {
 #endif
   }
   bool done = false;
-  if constexpr (FM % 2 == 0) {
+  if constexpr (HEAD) {
+    // every wave is past its last fragment read: the stages become the logit tile
+    __syncthreads();
+    float* T = reinterpret_cast<float*>(smem);
+    const int cob = wm * TM, pxb = wn * TN;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = cob + i * 16 + (lane >> 4) * 4 + r;
+        const float bv = co < a.Cout ? a.bias[co] : 0.0f;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) T[co * HEAD_LDT + pxb + j * 16 + (lane & 15)] = acc[i][j][r] + bv;
+      }
+    }
+    __syncthreads();
+    head_decode_tile<BN>(a, hd, T, HEAD_LDT, px0);
+    done = true;
+  }
+  if constexpr (FM % 2 == 0 && !HEAD) {
     if (perm) {
       epilogue_regs8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
       done = true;
     }
   }
-  if (!done) epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+  if (!HEAD && !done) epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
 #ifdef YCX_GLDS_STAMP
   {
     const unsigned long long e = stamp_issue();
@@ -2459,6 +2567,7 @@ const TileInfo kTiles[] = {
     {64, 128, 16, "f8_co64_px128_k128_s2"},
     {32, 64, 128, "f8_wres1x1"},
     {64, 256, 64, "f8_halo3x3_ws_co64"},
+    {256, 64, 64, "head_co256_px64_decode"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -2509,7 +2618,18 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   a.nsteps = TT ? (a.KH * a.KW + 1) / 2 : a.KH * a.KW * (a.Cin / 64);
   a.n_ct = a.Cout_pad / BM;
   a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST, NSB>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
+  hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST, NSB>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a,
+                     HeadArgs{});
+  return ycx_launch_status();
+}
+
+// tile 38: Detect head conv (all <= 256 channels of BN = 64 pixels per workgroup) + decode + filter
+ycx_status launch_head(ConvArgs a, const HeadArgs& hd, hipStream_t st) {
+  if (a.Cin % 64 || a.Cout_pad != 256 || a.Cout > 256) return YCX_ERR_UNSUPPORTED;
+  a.nsteps = a.KH * a.KW * (a.Cin / 64);
+  a.n_ct = 1;
+  a.nwg = (a.M + 63) / 64;
+  hipLaunchKernelGGL((conv_bf16_glds<256, 64, 4, 2, false, 2, 2, true>), dim3(a.nwg), dim3(512), 0, st, a, hd);
   return ycx_launch_status();
 }
 
@@ -2797,6 +2917,26 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
 #endif
     default: return YCX_ERR_UNSUPPORTED;
   }
+}
+
+extern "C" ycx_status ycx_conv2d_head(const ycx_conv_desc* d, const ycx_head_desc* h, const void* x, const void* w,
+                                      const float* bias, float* heads, ycx_cand* cand, int32_t* cand_rows,
+                                      int32_t* cand_counts, void* stream) {
+  YCX_CHECK_ARG(d && h && x && w && bias && cand && cand_rows && cand_counts);
+  YCX_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->cin > 0 && d->cout > 0 && d->ho == d->h && d->wo == d->w);
+  YCX_CHECK_ARG(d->in_c_off >= 0 && d->in_c_off + d->cin <= d->in_c_stride && d->cout_pad >= d->cout);
+  YCX_CHECK_ARG(h->na > 0 && h->na <= 8 && h->nc > 0 && h->no == h->nc + 5 && h->na * h->no == d->cout);
+  YCX_CHECK_ARG(h->row_off >= 0 && h->row_off + h->na * d->ho * d->wo <= h->rows_total);
+  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0);
+  YCX_CHECK_SUPPORTED(d->act == YCX_ACT_NONE && d->out_layout == YCX_OUT_NCHW_F32 && d->cout_pad == 256);
+  YCX_CHECK_SUPPORTED(d->in_c_off % 8 == 0 && d->in_c_stride % 8 == 0);
+  YCX_CHECK_SUPPORTED((long long)d->n * d->h * d->w * d->in_c_stride * 2 < (1LL << 31));
+  YCX_CHECK_SUPPORTED((long long)d->n * h->rows_total < (1LL << 31));
+  ConvArgs a = make_args(d, x, w, bias, heads, nullptr);
+  a.out_coff = 0;
+  a.out_cs = d->cout;
+  HeadArgs hd{*h, cand, cand_rows, cand_counts, heads};
+  return launch_head(a, hd, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, const float* w, const float* bias,

@@ -260,6 +260,9 @@ static ycx_status run_one(const ycx_op& op, void* stream) {
     case YCX_OP_STEM2:
       return ycx_stem_conv2(&op.d.pair[0], &op.d.pair[1], (const float*)op.in, (const float*)op.weight, op.bias,
                             op.weight2, op.bias2, op.out, stream);
+    case YCX_OP_HEAD:
+      return ycx_conv2d_head(&op.d.head.conv, &op.d.head.head, op.in, op.weight, op.bias, (float*)op.out,
+                             (ycx_cand*)op.cand, op.cand_rows, op.cand_counts, stream);
     default:
       return YCX_ERR_BAD_ARG;
   }
@@ -328,6 +331,7 @@ extern "C" size_t ycx_struct_size(int32_t which) {
     case 8: return sizeof(ycx_op);
     case 9: return sizeof(ycx_letterbox_desc);
     case 10: return sizeof(ycx_correct_desc);
+    case 11: return sizeof(ycx_head_desc);
     default: return 0;
   }
 }

@@ -18,14 +18,14 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see above)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("YCX_LIB", os.path.join(_HERE, "libycx_hip.so"))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # ---- enums (ycx.h) ----
 YCX_OK, YCX_ERR_BAD_ARG, YCX_ERR_UNSUPPORTED, YCX_ERR_LAUNCH, YCX_ERR_CAPACITY = 0, 1, 2, 3, 4
 DT_BF16, DT_F32, DT_FP8 = 0, 1, 2
 ACT_NONE, ACT_SILU, ACT_LEAKY = 0, 1, 2
 OUT_NHWC, OUT_NCHW_F32, OUT_NHWC_UP2 = 0, 1, 2
-OP_CONV, OP_STEM, OP_POOL, OP_COPY, OP_STEM2 = 1, 2, 3, 4, 5
+OP_CONV, OP_STEM, OP_POOL, OP_COPY, OP_STEM2, OP_HEAD = 1, 2, 3, 4, 5, 6
 
 _i32 = ctypes.c_int32
 
@@ -77,15 +77,26 @@ class NmsDesc(ctypes.Structure):
         ("iou_thres", ctypes.c_double)]
 
 
+class HeadDesc(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("na", "no", "nc", "rows_total", "row_off")] + [
+        ("conf_thres", ctypes.c_float), ("anchors_scaled", ctypes.c_float * 16)]
+
+
+class _HeadOp(ctypes.Structure):
+    _fields_ = [("conv", ConvDesc), ("head", HeadDesc)]
+
+
 class _OpUnion(ctypes.Union):
-    _fields_ = [("conv", ConvDesc), ("pool", PoolDesc), ("copy", CopyDesc), ("pair", ConvDesc * 2)]
+    _fields_ = [("conv", ConvDesc), ("pool", PoolDesc), ("copy", CopyDesc), ("pair", ConvDesc * 2),
+                ("head", _HeadOp)]
 
 
 class Op(ctypes.Structure):
     _fields_ = [("kind", _i32), ("pad_", _i32), ("d", _OpUnion),
                 ("in_", ctypes.c_void_p), ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p),
                 ("out", ctypes.c_void_p), ("residual", ctypes.c_void_p),
-                ("weight2", ctypes.c_void_p), ("bias2", ctypes.c_void_p)]
+                ("weight2", ctypes.c_void_p), ("bias2", ctypes.c_void_p),
+                ("cand", ctypes.c_void_p), ("cand_rows", ctypes.c_void_p), ("cand_counts", ctypes.c_void_p)]
 
 
 class LetterboxDesc(ctypes.Structure):
@@ -98,7 +109,7 @@ class CorrectDesc(ctypes.Structure):
 
 
 _STRUCTS = [ConvDesc, PoolDesc, CopyDesc, DecodeDesc, Cand, FilterDesc, DecodeFilterDesc, NmsDesc, Op, LetterboxDesc,
-            CorrectDesc]
+            CorrectDesc, HeadDesc]
 
 # (name, restype, argtypes) — every symbol declared in include/ycx.h.
 _VP = ctypes.c_void_p
@@ -109,6 +120,8 @@ _SIGS = [
     ("ycx_conv_tile_name", ctypes.c_char_p, [_i32]),
     ("ycx_conv_pick_tile", _i32, [ctypes.POINTER(ConvDesc)]),
     ("ycx_conv2d", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP]),
+    ("ycx_conv2d_head", _i32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(HeadDesc), _VP, _VP, _VP, _VP, _VP, _VP,
+                               _VP, _VP]),
     ("ycx_stem_conv", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP]),
     ("ycx_idetect_decode", _i32, [ctypes.POINTER(DecodeDesc), ctypes.c_float, _VP, _VP, _VP, _VP]),
     ("ycx_letterbox", _i32, [ctypes.POINTER(LetterboxDesc), _VP, _VP, _VP]),

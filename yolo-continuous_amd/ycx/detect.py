@@ -206,7 +206,10 @@ class DevicePost:
 
     Outputs stay on device: dets [n, max_det, 7] (normalised xyxy, obj,
     cls_conf, cls), keep_rows [n, max_det] (row into the concatenated
-    [sum na*H*W] candidates, -1 padded), keep_counts [n] (uncapped)."""
+    [sum na*H*W] candidates, -1 padded), keep_counts [n] (uncapped).
+
+    ``fused`` (set by a Detector whose plan decodes in the head convs): the
+    candidates are already written by the forward, a call runs the NMS only."""
 
     def __init__(self, heads, nc, anchors, anchors_mask, image_size, device, conf_thres=0.3, nms_thres=0.3,
                  max_det=300):
@@ -216,10 +219,12 @@ class DevicePost:
             if hd.dtype != torch.float32 or not hd.is_contiguous():
                 raise ValueError("ycx: DevicePost needs contiguous fp32 heads")
         self.heads = heads
+        self.fused = False
         n = heads[0].shape[0]
         d = L.DecodeFilterDesc()
         d.n, d.nl, d.na, d.no, d.nc = n, len(heads), len(anchors_mask[0]), nc + 5, nc
         off = 0
+        self.level_descs = []
         for l, hd in enumerate(heads):
             h, w = hd.shape[2], hd.shape[3]
             if hd.shape[0] != n or hd.shape[1] != d.na * d.no:
@@ -230,6 +235,13 @@ class DevicePost:
                 d.anchors_scaled[l][2 * a], d.anchors_scaled[l][2 * a + 1] = aw[a], ah[a]
             off += len(anchors_mask[l]) * h * w
         d.rows_total, d.conf_thres = off, float(conf_thres)
+        for l in range(len(heads)):  # the same level parameters for the fused head convs
+            hdsc = L.HeadDesc()
+            hdsc.na, hdsc.no, hdsc.nc, hdsc.rows_total, hdsc.row_off = d.na, d.no, nc, off, d.row_off[l]
+            hdsc.conf_thres = d.conf_thres
+            for k in range(2 * d.na):
+                hdsc.anchors_scaled[k] = d.anchors_scaled[l][k]
+            self.level_descs.append(hdsc)
         self.rows = off
         self.df_desc = d
         self.heads_arr = (ctypes.c_void_p * 4)(*[h.data_ptr() for h in heads], *([None] * (4 - len(heads))))
@@ -245,9 +257,11 @@ class DevicePost:
 
     def __call__(self):
         st = L.stream_handle(self.device)
-        self.counts.zero_()
-        L.check(L.lib.ycx_decode_filter(ctypes.byref(self.df_desc), self.heads_arr, self.cand.data_ptr(),
-                                        self.cand_rows.data_ptr(), self.counts.data_ptr(), st), "ycx_decode_filter")
+        if not self.fused:
+            self.counts.zero_()
+            L.check(L.lib.ycx_decode_filter(ctypes.byref(self.df_desc), self.heads_arr, self.cand.data_ptr(),
+                                            self.cand_rows.data_ptr(), self.counts.data_ptr(), st),
+                    "ycx_decode_filter")
         L.check(L.lib.ycx_sort_nms(ctypes.byref(self.nms_desc), self.cand.data_ptr(), self.cand_rows.data_ptr(),
                                    self.counts.data_ptr(), self.ws.data_ptr(), self.ws_bytes, self.dets.data_ptr(),
                                    self.keep.data_ptr(), self.kc.data_ptr(), st), "ycx_sort_nms")
@@ -256,14 +270,21 @@ class DevicePost:
 
 class Detector:
     """Fused device pipeline for a fixed batch shape: Model forward (static plan,
-    optionally one HIP graph) -> ycx_decode_filter -> ycx_sort_nms (DevicePost).
+    optionally one HIP graph) -> candidates -> ycx_sort_nms (DevicePost).
+
+    bf16 Detect models decode in the head convs (``fuse_heads``, default): each
+    head level's ycx_conv2d_head appends that level's candidates straight from
+    the fp32 logits held on chip (detect.py:29-121), so the forward ends with
+    the candidate list and the post is the NMS alone. ``keep_heads`` also
+    stores the raw fp32 NCHW logits in ``self.heads`` (the parity tests read
+    them; bench.py turns it off). Other plans run ycx_decode_filter in post().
 
     Outputs stay on device: dets [n, max_det, 7] (normalised xyxy, obj,
     cls_conf, cls), keep_rows [n, max_det] (row into the concatenated
     [sum na*H*W] candidates, -1 padded), keep_counts [n] (uncapped)."""
 
     def __init__(self, model, shape, device, anchors, anchors_mask, image_size=None, conf_thres=0.3,
-                 nms_thres=0.3, max_det=300, use_graph=True, slot=None):
+                 nms_thres=0.3, max_det=300, use_graph=True, slot=None, fuse_heads=True, keep_heads=True):
         self.model = model
         # a private engine unless the caller names a slot: the static buffers of one
         # Detector must never alias model(x)'s or another Detector's (in flight on
@@ -281,6 +302,10 @@ class Detector:
         for k in ("rows", "df_desc", "cand", "cand_rows", "counts", "nms_desc", "ws_bytes", "ws", "dets", "keep",
                   "kc"):
             setattr(self, k, getattr(self._post, k))
+        self.fused = bool(fuse_heads) and self.engine.enable_head_decode(
+            self._post.level_descs, self.cand, self.cand_rows, self.counts, keep_heads=keep_heads)
+        self._post.fused = self.fused
+        self.keep_heads = keep_heads or not self.fused
         self.use_graph = use_graph
         if use_graph:
             self.engine.capture()
@@ -289,7 +314,10 @@ class Detector:
         return self._post()
 
     def forward(self, events=None):
-        """The model forward on the static input buffer (current stream)."""
+        """The model forward on the static input buffer (current stream); with
+        fused heads it also produces this batch's candidates."""
+        if self.fused:
+            self.counts.zero_()
         if self.use_graph and events is None:
             self.engine.replay()
         else:

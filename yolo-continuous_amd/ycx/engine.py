@@ -567,6 +567,8 @@ class Engine:
                 raise AssertionError(k)
         self.n_ops = len(ops)
         self.ops = (L.Op * max(1, self.n_ops))(*ops)
+        self.head_params = []
+        self.head_unstored = set()  # fused head ops that do not store raw logits (enable_head_decode)
         self.fixed_outputs = None
         self.static_input = None
         self._static_bound = False
@@ -719,7 +721,61 @@ class Engine:
     def _bind_outputs(self, outs):
         for v, t in zip(self.out_vals, outs):
             for idx, field in self.output_slots.get(id(v), []):
-                setattr(self.ops[idx], field, t.data_ptr())
+                setattr(self.ops[idx], field, None if idx in self.head_unstored else t.data_ptr())
+
+    # ---- fused Detect heads (decode + candidate filter in the head conv) ----
+    def head_ops(self):
+        """Op index of each output's producing conv, when every output is a bf16
+        Detect-head 1x1 conv the fused kernel covers (ycx_conv2d_head), else None."""
+        if self.dt != L.DT_BF16:
+            return None
+        idx = []
+        for v in self.out_vals:
+            slots = self.output_slots.get(id(v), [])
+            if len(slots) != 1 or slots[0][1] != 'out':
+                return None
+            op = self.ops[slots[0][0]]
+            d = op.d.conv
+            if not (op.kind == L.OP_CONV and d.kh == 1 and d.kw == 1 and d.stride == 1 and d.pad == 0 and
+                    d.act == L.ACT_NONE and d.out_layout == L.OUT_NCHW_F32 and d.cout <= 256 and
+                    d.cin % 64 == 0 and d.in_c_off % 8 == 0 and d.in_c_stride % 8 == 0):
+                return None
+            idx.append(slots[0][0])
+        return idx
+
+    def enable_head_decode(self, head_descs, cand, cand_rows, counts, keep_heads=True):
+        """Turn the Detect-head convs into ycx_conv2d_head ops (decode_box + the
+        candidate filter of detect.py:29-121 in the conv epilogue; candidates
+        appended to cand / cand_rows / counts, which the caller zeroes before
+        every forward). keep_heads: also store the raw fp32 NCHW logits.
+        Must precede capture(). Returns False when the plan does not qualify."""
+        if self.graph_exec is not None:
+            raise RuntimeError("ycx: enable_head_decode() after capture()")
+        idx = self.head_ops()
+        if idx is None or len(head_descs) != len(idx):
+            return False
+        for i, hd in zip(idx, head_descs):
+            op = self.ops[i]
+            conv = L.ConvDesc()
+            ctypes.pointer(conv)[0] = op.d.conv
+            if conv.cout_pad != 256:  # the head tile covers 256 output channels: zero-pad the weight rows
+                wi = next(j for j, t in enumerate(self.params) if t.data_ptr() == op.weight)
+                w, b = self.params[wi], self.params[wi + 1]
+                w2 = torch.zeros((256,) + tuple(w.shape[1:]), dtype=w.dtype, device=w.device)
+                b2 = torch.zeros((256,), dtype=b.dtype, device=b.device)
+                w2[:conv.cout], b2[:conv.cout] = w[:conv.cout], b[:conv.cout]
+                self.head_params += [w2, b2]   # self.params keeps the plan's shapes (prepack)
+                op.weight, op.bias, conv.cout_pad = w2.data_ptr(), b2.data_ptr(), 256
+            op.kind = L.OP_HEAD
+            op.d.head.conv = conv
+            op.d.head.head = hd
+            op.cand, op.cand_rows, op.cand_counts = cand.data_ptr(), cand_rows.data_ptr(), counts.data_ptr()
+            self.op_info[i] = dict(self.op_info[i], name=L.lib.ycx_conv_tile_name(38).decode(), kind='head')
+            if not keep_heads:
+                self.head_unstored.add(i)
+        if self.fixed_outputs is not None:
+            self._bind_outputs(self.fixed_outputs)
+        return True
 
     def _bind_input(self, x):
         if x.device != self.device or x.dtype != torch.float32 or not x.is_contiguous():
