@@ -278,6 +278,12 @@ ycx_status ycx_filter_decoded(const ycx_filter_desc* d, float* pred, ycx_cand* c
                               int32_t* cand_rows, int32_t* cand_counts, void* stream);
 ycx_status ycx_decode_filter(const ycx_decode_filter_desc* d, const float* const* heads,
                              ycx_cand* cand, int32_t* cand_rows, int32_t* cand_counts, void* stream);
+/* Device self-check behind the class scan of the decode filters (no reference
+ * counterpart): adds to *violations (device uint64, caller-zeroed) the number of
+ * adjacent finite-float pairs x < y with sigmoid(x) > sigmoid(y) for the
+ * decoders' sigmoid, over every float. The filters' exact class argmax relies
+ * on it being 0 (ycx_internal.h, ycx_class_argmax). */
+ycx_status ycx_check_sigmoid_monotone(unsigned long long* violations, void* stream);
 size_t ycx_nms_workspace_size(const ycx_nms_desc* d);
 /* Sorts each image's candidates by (class asc, score desc, row asc) — the order
  * of detect.py:124-137 with a stable torchvision sort — and runs greedy NMS per

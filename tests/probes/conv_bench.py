@@ -42,6 +42,9 @@ SHAPES = [  # n, h, w, cin, cout, k, s
     (32, 20, 20, 512, 1024, 3, 1),
     (32, 40, 40, 256, 512, 3, 1),
 ]
+# CONV_EXTRA="64,32,32,4096,4096,1,1;32,40,40,1024,1024,1,1": extra shapes appended (indices continue)
+for _s in filter(None, os.environ.get("CONV_EXTRA", "").split(";")):
+    SHAPES.append(tuple(int(v) for v in _s.split(",")))
 
 
 def run(shape, tile, iters=20):

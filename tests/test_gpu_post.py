@@ -133,6 +133,87 @@ def test_device_post_sparse_class_ties(device, scalar, monkeypatch):
     assert {0, 3, 79} <= set(dets[0, :int(kc[0]), 6].cpu().long().tolist())
 
 
+def test_sigmoid_monotone_every_float(device):
+    """The decoders' sigmoid is monotone non-decreasing over all 2^32 floats
+    (ycx_check_sigmoid_monotone): the premise of the exact class argmax
+    (ycx_internal.h ycx_class_argmax) that reads nc logits and a few sigmoids."""
+    import ctypes
+    from ycx import _lib as L
+    bad = torch.zeros(1, dtype=torch.int64, device=device)
+    L.check(L.lib.ycx_check_sigmoid_monotone(ctypes.c_void_p(bad.data_ptr()), L.stream_handle(device)),
+            "ycx_check_sigmoid_monotone")
+    torch.cuda.synchronize()
+    assert int(bad) == 0
+
+
+@pytest.mark.parametrize('scalar', [True, False])
+def test_device_post_dense_class_scan(device, scalar, monkeypatch):
+    """Dense waves (every row passes on objectness) with crafted class logits:
+    saturated ties (several logits past ~17 give sigmoid 1.0: first such class),
+    exact ties, near-ties one float apart, +inf, -inf and NaN (class 0 NaN sticks,
+    later NaNs never win). Every candidate's (cls, cls_conf) equals the
+    sequential strict-'>' scan over the device's own sigmoids (ycx_decode),
+    i.e. the exact class argmax is the scan bit for bit."""
+    if scalar:
+        monkeypatch.setenv('YCX_DECODE_SCALAR', '1')
+    nc, bs, size = 80, 2, 320
+    g = torch.Generator().manual_seed(11)
+    shapes = [(size // k, size // k) for k in (32, 16, 8)]
+    heads = [torch.randn(bs, 3, 5 + nc, h, w, generator=g) * 3.0 for h, w in shapes]
+    rng = np.random.default_rng(7)
+    for hd in heads:
+        hd[:, :, 4] = 6.0
+        flat = hd.permute(0, 1, 3, 4, 2).reshape(-1, 5 + nc)   # view: rows x channels
+        for r in rng.choice(flat.shape[0], size=flat.shape[0] // 2, replace=False):
+            kind = int(rng.integers(8))
+            ks = rng.choice(nc, size=3, replace=False)
+            if kind == 0:
+                flat[r, 5 + ks] = torch.tensor([18.0, 25.0, 40.0])          # saturated: all 1.0
+            elif kind == 1:
+                flat[r, 5 + ks] = 4.25                                       # exact tie
+            elif kind == 2:
+                v = np.float32(2.5)
+                flat[r, 5 + ks[0]] = float(v)
+                flat[r, 5 + ks[1]] = float(np.nextafter(v, np.float32(0)))   # one float below
+                flat[r, 5 + ks[2]] = float(np.nextafter(v, np.float32(9)))   # one float above
+            elif kind == 3:
+                flat[r, 5 + ks[0]] = float('inf')
+                flat[r, 5 + ks[1]] = 30.0
+            elif kind == 4:
+                flat[r, 5 + ks[0]] = float('-inf')
+            elif kind == 5:
+                flat[r, 5 + ks[0]] = float('nan')
+                flat[r, 5 + ks[1]] = 9.0
+            elif kind == 6:
+                flat[r, 5] = float('nan')                                    # class 0 NaN sticks
+            else:
+                flat[r, 5 + ks] = torch.tensor([16.5, 16.6, 16.7])           # edge of saturation
+        hd.copy_(flat.reshape(hd.shape[0], hd.shape[1], hd.shape[3], hd.shape[4], 5 + nc).permute(0, 1, 4, 2, 3))
+    heads = [hd.reshape(bs, 3 * (5 + nc), h, w).contiguous() for hd, (h, w) in zip(heads, shapes)]
+    dh = [h.to(device) for h in heads]
+    post = DevicePost(dh, nc, ANCHORS, MASK, (size, size), device, 0.0, 0.45, 100)
+    post.counts.zero_()
+    post()
+    dec = torch.cat(decode_box(dh, A, MASK, nc, (size, size)), 1).cpu().numpy()
+    torch.cuda.synchronize()
+    cls_sig = dec[..., 5:]
+    for b in range(bs):
+        n = int(post.counts[b])
+        rows = np.sort(post.cand_rows[b, :n].cpu().numpy())
+        cand = post.cand[b].cpu().numpy()[rows]
+        sig = cls_sig[b, rows]
+        want_i = np.zeros(len(rows), dtype=np.int64)
+        want_v = sig[:, 0].copy()
+        for k in range(1, nc):   # the sequential scan of detect.py:109 as the kernels define it
+            upd = sig[:, k] > want_v
+            want_v[upd] = sig[upd, k]
+            want_i[upd] = k
+        got_i = cand[:, 6].view(np.int32)
+        np.testing.assert_array_equal(got_i, want_i)
+        np.testing.assert_array_equal(cand[:, 5].view(np.uint32), want_v.view(np.uint32))
+        assert n > 0.4 * dec.shape[1]
+
+
 @pytest.mark.parametrize('name', CASES)
 def test_non_max_suppression_final(device, manifest, g3, name):
     e = manifest['g3'][name]

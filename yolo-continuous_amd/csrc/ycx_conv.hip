@@ -365,15 +365,26 @@ __device__ __forceinline__ void epilogue_frag8(const ConvArgs& a, const f32x4 (&
 // NHWC epilogue for permuted A rows (conv_bf16_glds): fragments 2k, 2k+1 hold channels
 // cob + 32k + 8g .. +7 in C rows 4g..4g+3 (g = lane >> 4): one 16-byte store per lane and pixel
 // (store8: residual and x2 upsample included).
+// bias8_prefetch loads the bias of these channels (bias is [cout_pad]: always in bounds)
+// before the K loop, so the epilogue does not wait on a load round trip per fragment pair.
+template <int FM>
+__device__ __forceinline__ void bias8_prefetch(const ConvArgs& a, int cob, int lane, f32x4 (&bp)[FM]) {
+#pragma unroll
+  for (int k = 0; k < FM / 2; ++k) {
+    const int co = cob + 32 * k + 8 * (lane >> 4);
+    bp[2 * k] = *reinterpret_cast<const f32x4*>(a.bias + co);
+    bp[2 * k + 1] = *reinterpret_cast<const f32x4*>(a.bias + co + 4);
+  }
+}
+
 template <int FM, int FN>
 __device__ __forceinline__ void epilogue_regs8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob, int pxb,
-                                               int lane) {
+                                               int lane, const f32x4 (&bp)[FM]) {
 #pragma unroll
   for (int k = 0; k < FM / 2; ++k) {
     const int co = cob + 32 * k + 8 * (lane >> 4);
     if (co >= a.Cout) continue;  // cout % 8 == 0: the 8 channels are all valid
-    const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + co);
-    const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bias + co + 4);
+    const f32x4 b0 = bp[2 * k], b1 = bp[2 * k + 1];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int p = pxb + j * 16 + (lane & 15);
@@ -459,10 +470,7 @@ struct HeadArgs {
   float* heads;
 };
 
-__device__ __forceinline__ float head_sigmoid(float v) {
-#pragma clang fp contract(off)
-  return 1.0f / (1.0f + expf(-v));
-}
+__device__ __forceinline__ float head_sigmoid(float v) { return ycx_sigmoid(v); }
 
 template <int BN>
 __device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const float* T, int ldt, int px0) {
@@ -479,54 +487,126 @@ __device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const fl
       }
     }
   }
-  for (int it = tid; it < ((h.na * BN + 63) & ~63); it += blockDim.x) {  // whole waves: appends are wave-wide
-    const int an = it / BN, px = it - an * BN, p = px0 + px;
-    const bool valid = an < h.na && p < a.M;
-    const int n = valid ? p / HW : 0, cell = valid ? p - n * HW : 0;
-    bool pass = false;
-    ycx_cand c;
+  // One thread per row an * BN + px (kSplit, measured slower on MI355X: lanes l and l + 32
+  // scan the lower and upper half of one row's classes, the lower lane finishes the row).
+#ifdef YCX_HEAD_SPLIT
+  constexpr bool kSplit = true;
+#else
+  constexpr bool kSplit = false;
+#endif
+  const int wid = tid >> 6, upper = kSplit ? lane >> 5 : 0, nrows = h.na * BN;
+  const int per = kSplit ? blockDim.x / 2 : blockDim.x;
+  const int n0 = px0 / HW;
+  const bool two = min(px0 + BN, a.M) - 1 < (n0 + 2) * HW;  // the tile spans one or two images
+  const float inv_w = 1.0f / (float)W;
+  int* s_cnt = reinterpret_cast<int*>(const_cast<float*>(T) + a.Cout_pad * ldt);  // [16][2] + [2], past the tile
+  for (int r0 = 0; r0 < nrows; r0 += per) {  // uniform trip count
+    const int r = r0 + (kSplit ? wid * 32 + (lane & 31) : tid);
+    const int an = r / BN, px = r - an * BN, p = px0 + px;
+    const bool valid = r < nrows && p < a.M;
+    int n = 0, cell = 0;
     if (valid) {
-      const float* L = T + (size_t)(an * h.no) * ldt + px;
-      const float obj = head_sigmoid(L[4 * ldt]);
-      if (obj >= h.conf_thres) {  // obj * cls <= obj: otherwise the row cannot pass
-        float best = head_sigmoid(L[5 * ldt]);
-        int bi = 0;
-        for (int k = 1; k < h.nc; ++k) {
-          const float sv = head_sigmoid(L[(5 + k) * ldt]);
-          if (sv > best) { best = sv; bi = k; }
-        }
-        const float score = obj * best;
-        if (score >= h.conf_thres) {
-          const float gx = (float)(cell % W), gy = (float)(cell / W);
-          const float px_ = head_sigmoid(L[0]), py = head_sigmoid(L[ldt]);
-          const float pw = head_sigmoid(L[2 * ldt]), ph = head_sigmoid(L[3 * ldt]);
-          const float bx = ((px_ * 2.0f) - 0.5f + gx) / (float)W;
-          const float by = ((py * 2.0f) - 0.5f + gy) / (float)H;
-          const float tw = pw * 2.0f, th = ph * 2.0f;
-          const float bw = (tw * tw * h.anchors_scaled[2 * an]) / (float)W;
-          const float bhh = (th * th * h.anchors_scaled[2 * an + 1]) / (float)H;
-          pass = true;
-          c = ycx_cand{bx - bw / 2.0f, by - bhh / 2.0f, bx + bw / 2.0f, by + bhh / 2.0f, obj, best, bi,
-                       h.row_off + an * HW + cell};
-        }
+      n = p >= (n0 + 1) * HW ? (two ? n0 + 1 : p / HW) : n0;
+      cell = p - n * HW;
+    }
+    const float* L = T + (size_t)(an * h.no) * ldt + px;
+    const float obj = valid ? head_sigmoid(L[4 * ldt]) : 0.0f;
+    const bool want = valid && obj >= h.conf_thres;  // obj * cls <= obj: otherwise the row cannot pass
+    auto logit = [&](int k) { return L[(5 + k) * ldt]; };
+    const int c = kSplit ? h.nc >> 1 : h.nc;
+    float m = -INFINITY, pm = -INFINITY;
+    int b = -1;
+    if (want) {
+      if (kSplit && upper) {
+        ycx_class_scan(logit, c, h.nc, m, pm, b);
+      } else if (kSplit) {
+        m = logit(0);
+        b = 0;
+        ycx_class_scan(logit, 1, c, m, pm, b);
+      } else {
+        ycx_class_scan2(logit, h.nc, m, pm, b);
       }
     }
-    // wave-aggregated append per image (a tile spans at most a few images)
+    float m2 = -INFINITY, pm2 = -INFINITY;
+    int b2 = -1;
+    if constexpr (kSplit) {
+      m2 = __shfl_xor(m, 32);
+      pm2 = __shfl_xor(pm, 32);
+      b2 = __shfl_xor(b, 32);
+    }
+    bool pass = false;
+    ycx_cand cd;
+    if (want && !upper) {
+      float best;
+      int bi;
+      if (m != m) {  // NaN at class 0 sticks (the sequential scan's 'sv > NaN' never holds)
+        best = m;
+        bi = 0;
+      } else {
+        ycx_class_merge(m, pm, b, m2, pm2, b2);
+        ycx_class_finish(logit, m, pm, b, best, bi);
+      }
+      const float score = obj * best;
+      if (score >= h.conf_thres) {
+        int iy = (int)((float)cell * inv_w);  // cell / W: exact after the +-1 fix-up (cell < 2^24)
+        iy -= iy * W > cell ? 1 : 0;
+        iy += (iy + 1) * W <= cell ? 1 : 0;
+        const float gx = (float)(cell - iy * W), gy = (float)iy;
+        const float px_ = head_sigmoid(L[0]), py = head_sigmoid(L[ldt]);
+        const float pw = head_sigmoid(L[2 * ldt]), ph = head_sigmoid(L[3 * ldt]);
+        const float bx = ((px_ * 2.0f) - 0.5f + gx) / (float)W;
+        const float by = ((py * 2.0f) - 0.5f + gy) / (float)H;
+        const float tw = pw * 2.0f, th = ph * 2.0f;
+        const float bw = (tw * tw * h.anchors_scaled[2 * an]) / (float)W;
+        const float bhh = (th * th * h.anchors_scaled[2 * an + 1]) / (float)H;
+        pass = true;
+        cd = ycx_cand{bx - bw / 2.0f, by - bhh / 2.0f, bx + bw / 2.0f, by + bhh / 2.0f, obj, best, bi,
+                      h.row_off + an * HW + cell};
+      }
+    }
+    if (two) {  // one atomic per (block, image) instead of one per (wave, image)
+      const int k = n - n0;
+      const unsigned long long q0 = __ballot(pass && k == 0), q1 = __ballot(pass && k == 1);
+      if (lane == 0) {
+        s_cnt[2 * wid] = __popcll(q0);
+        s_cnt[2 * wid + 1] = __popcll(q1);
+      }
+      __syncthreads();
+      if (tid < 2) {
+        int tot = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += s_cnt[2 * w + tid];
+#ifndef YCX_HEAD_NOATOMIC  // development A/B only (slots = rows: wrong counts)
+        s_cnt[32 + tid] = tot ? atomicAdd(hd.counts + n0 + tid, tot) : 0;
+#else
+        s_cnt[32 + tid] = 0;
+#endif
+      }
+      __syncthreads();
+      if (pass) {
+        int slot = s_cnt[32 + k] + __popcll((k ? q1 : q0) & ((1ull << lane) - 1ull));
+        for (int w = 0; w < wid; ++w) slot += s_cnt[2 * w + k];
+        hd.cand[(size_t)n * h.rows_total + cd.row] = cd;
+        hd.rows_out[(size_t)n * h.rows_total + slot] = cd.row;
+      }
+      __syncthreads();  // s_cnt is reused by the next pass
+      continue;
+    }
+    // tiny maps (a tile over three or more images): wave-aggregated append per image
     unsigned long long rem = __ballot(pass);
     while (rem) {
       const int leader = __ffsll((long long)rem) - 1;
       const int nl = __shfl(n, leader);
       const bool mine = pass && n == nl;
-      const unsigned long long m = __ballot(mine);
+      const unsigned long long q = __ballot(mine);
       int base = 0;
-      if (lane == leader) base = atomicAdd(hd.counts + nl, __popcll(m));
+      if (lane == leader) base = atomicAdd(hd.counts + nl, __popcll(q));
       base = __shfl(base, leader);
       if (mine) {
-        const int slot = base + __popcll(m & ((1ull << lane) - 1ull));
-        hd.cand[(size_t)nl * h.rows_total + c.row] = c;
-        hd.rows_out[(size_t)nl * h.rows_total + slot] = c.row;
+        const int slot = base + __popcll(q & ((1ull << lane) - 1ull));
+        hd.cand[(size_t)nl * h.rows_total + cd.row] = cd;
+        hd.rows_out[(size_t)nl * h.rows_total + slot] = cd.row;
       }
-      rem &= ~m;
+      rem &= ~q;
     }
   }
 }
@@ -557,7 +637,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   constexpr int LDS_BYTES = SPLIT ? NST * A_BYTES + NSB * B_BYTES : NST * STAGE;
   static_assert(A_PW >= 1 && B_PW >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows per wave");
   constexpr int HEAD_LDT = BN + 1;  // HEAD: fp32 logits [BM][BN + 1] (odd stride: conflict-free writes)
-  static_assert(!HEAD || BM * HEAD_LDT * 4 <= LDS_BYTES, "head tile fits the stages");
+  static_assert(!HEAD || BM * HEAD_LDT * 4 + 34 * 4 <= LDS_BYTES, "head tile (+ append counts) fits the stages");
+  static_assert(!HEAD || NW <= 16, "head append counts: 16 waves");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
   const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
@@ -656,6 +737,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // epilogue bias in registers before the K loop (a load round trip per fragment pair otherwise)
+  f32x4 bpre[FM];
+  if constexpr (HEAD) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) bpre[i] = *reinterpret_cast<const f32x4*>(a.bias + co0 + wm * TM + i * 16 + (lane >> 4) * 4);
+  } else if constexpr (FM % 2 == 0) {
+    if (perm) bias8_prefetch<FM>(a, co0 + wm * TM, lane, bpre);
+  }
   const int nt = a.nsteps;
   if constexpr (SPLIT) {
     // prologue A0, B0, B1; step t issues A(t+1) then B(t+2), so at the top of step t the
@@ -745,18 +834,19 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = cob + i * 16 + (lane >> 4) * 4 + r;
-        const float bv = co < a.Cout ? a.bias[co] : 0.0f;
 #pragma unroll
-        for (int j = 0; j < FN; ++j) T[co * HEAD_LDT + pxb + j * 16 + (lane & 15)] = acc[i][j][r] + bv;
+        for (int j = 0; j < FN; ++j) T[co * HEAD_LDT + pxb + j * 16 + (lane & 15)] = acc[i][j][r] + bpre[i][r];
       }
     }
     __syncthreads();
+#ifndef YCX_HEAD_NODECODE  // development A/B only: conv + logit tile without the decode
     head_decode_tile<BN>(a, hd, T, HEAD_LDT, px0);
+#endif
     done = true;
   }
   if constexpr (FM % 2 == 0 && !HEAD) {
     if (perm) {
-      epilogue_regs8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+      epilogue_regs8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane, bpre);
       done = true;
     }
   }

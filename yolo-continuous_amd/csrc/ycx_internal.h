@@ -52,3 +52,123 @@ __device__ __forceinline__ int ycx_xcd_remap(int bid, int nwg) {
   int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
+
+// torch.sigmoid as the decode kernels evaluate it (detect.py:53, 1/(1+e^-v),
+// IEEE division, no contraction possible). One definition for every kernel
+// that must produce bit-identical candidates.
+__device__ __forceinline__ float ycx_sigmoid(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+// The class scan of detect.py:109-110 (torch.max over sigmoid(class logits),
+// first index on ties) as the sequential strict-'>' scan defines it, with one
+// pass of compares over the logits and two sigmoids instead of nc sigmoids.
+// logit(k) returns class k's raw logit. ycx_sigmoid is monotone
+// non-decreasing over every float (checked exhaustively on the device:
+// ycx_check_sigmoid_monotone, tests/test_gpu_post.py). With m the largest
+// non-NaN logit, bi its first index and pm the largest logit before bi: the
+// scan's maximum is sm = sigmoid(m), and a class before bi can tie it only
+// with a logit in [lo, m), where sigmoid(lo) < sm; so unless pm >= lo (a
+// saturated or one-ulp tie, rare) the answer is bi. A NaN at class 0 sticks
+// (the scan's 'sv > NaN' never holds); other NaNs never win.
+// Running (m, first index b, largest logit before b) over classes [k0, k1).
+// Start from m = -inf, b = -1 (empty) or from class 0's logit (m = l0, b = 0).
+template <class F>
+__device__ __forceinline__ void ycx_class_scan(F&& logit, int k0, int k1, float& m, float& pm, int& b) {
+  int k = k0;
+  for (; k + 8 <= k1; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = logit(k + u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool up = v[u] > m;  // false for NaN
+      pm = up ? m : pm;
+      b = up ? k + u : b;
+      m = up ? v[u] : m;
+    }
+  }
+  for (; k < k1; ++k) {
+    const float v = logit(k);
+    const bool up = v > m;
+    pm = up ? m : pm;
+    b = up ? k : b;
+    m = up ? v : m;
+  }
+}
+
+// (m, pm, b) of a lower part [0, c) and an upper part [c, nc) -> those of [0, nc).
+__device__ __forceinline__ void ycx_class_merge(float& m, float& pm, int& b, float m2, float pm2, int b2) {
+  if (m2 > m) {  // the upper part's maximum is larger: everything below c precedes it
+    pm = fmaxf(m, pm2);
+    m = m2;
+    b = b2;
+  }
+}
+
+// From the scan state of all classes (l0 not NaN) to the sequential scan's answer.
+template <class F>
+__device__ __forceinline__ void ycx_class_finish(F&& logit, float m, float pm, int b, float& best, int& bi) {
+  const float sm = ycx_sigmoid(m);
+  best = sm;
+  bi = b;
+  if (pm == -INFINITY) return;  // nothing before bi can reach sm
+  float tau = fmaxf(fabsf(m), 1.0f) * 0x1p-12f, lo = m < INFINITY ? m - tau : -INFINITY;
+  for (int i = 0; i < 6 && ycx_sigmoid(lo) == sm; ++i) {  // saturated: widen until sigmoid drops
+    tau *= 16.0f;
+    lo = m - tau;
+  }
+  if (ycx_sigmoid(lo) == sm) lo = -INFINITY;  // still tied: every class is a candidate
+  if (!(pm >= lo)) return;
+  for (int k = 0; k < b; ++k) {  // rare: a class before bi whose sigmoid rounds to sm
+    const float v = logit(k);
+    if (v >= lo && ycx_sigmoid(v) == sm) {
+      bi = k;
+      return;
+    }
+  }
+}
+
+// Both halves of the classes as two independent chains (twice the ILP of one scan).
+template <class F>
+__device__ __forceinline__ void ycx_class_scan2(F&& logit, int nc, float& m, float& pm, int& b) {
+  const int c = nc >> 1;
+  float m2 = -INFINITY, pm2 = -INFINITY;
+  int b2 = -1, k = 1, k2 = c;
+  m = logit(0);
+  pm = -INFINITY;
+  b = 0;
+  for (; k + 4 <= c && k2 + 4 <= nc; k += 4, k2 += 4) {
+    float v[4], w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[u] = logit(k + u);
+      w[u] = logit(k2 + u);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool up = v[u] > m, up2 = w[u] > m2;
+      pm = up ? m : pm;
+      b = up ? k + u : b;
+      m = up ? v[u] : m;
+      pm2 = up2 ? m2 : pm2;
+      b2 = up2 ? k2 + u : b2;
+      m2 = up2 ? w[u] : m2;
+    }
+  }
+  ycx_class_scan(logit, k, c, m, pm, b);
+  ycx_class_scan(logit, k2, nc, m2, pm2, b2);
+  ycx_class_merge(m, pm, b, m2, pm2, b2);
+}
+
+template <class F>
+__device__ __forceinline__ void ycx_class_argmax(F&& logit, int nc, float& best, int& bi) {
+  const float l0 = logit(0);
+  if (l0 != l0) {
+    best = l0;
+    bi = 0;
+    return;
+  }
+  float m, pm;
+  int b;
+  ycx_class_scan2(logit, nc, m, pm, b);
+  ycx_class_finish(logit, m, pm, b, best, bi);
+}

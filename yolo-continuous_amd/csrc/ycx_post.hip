@@ -17,7 +17,7 @@
 
 namespace {
 
-__device__ __forceinline__ float sigmoidf_ref(float v) { return 1.0f / (1.0f + expf(-v)); }
+__device__ __forceinline__ float sigmoidf_ref(float v) { return ycx_sigmoid(v); }
 
 // Wave-aggregated append: one atomic per wave (ballot + popcount + mbcnt).
 __device__ __forceinline__ int wave_append(bool pass, int* counter) {
@@ -233,24 +233,7 @@ __global__ void __launch_bounds__(256) decode_filter_kernel(DecodeFilterArgs a, 
       }
     }
   } else if (want) {
-    best = sigmoidf_ref(hb[(size_t)5 * hw]);
-    int k = 1;
-    // eight class logits in flight per thread (a load-use chain per class left the kernel
-    // latency-bound at ~0.8 TB/s); the compares stay in class order (first index on ties)
-    for (; k + 8 <= d.nc; k += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = hb[(size_t)(5 + k + u) * hw];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float sv = sigmoidf_ref(v[u]);
-        if (sv > best) { best = sv; bi = k + u; }
-      }
-    }
-    for (; k < d.nc; ++k) {
-      float v = sigmoidf_ref(hb[(size_t)(5 + k) * hw]);
-      if (v > best) { best = v; bi = k; }
-    }
+    ycx_class_argmax([&](int k) { return hb[(size_t)(5 + k) * hw]; }, d.nc, best, bi);
   }
   if (want) {
     const float score = obj * best;
@@ -430,6 +413,34 @@ __global__ void __launch_bounds__(256) decode_filter4_kernel(DecodeFilterArgs a,
 }
 
 }  // namespace
+
+namespace {
+// Every finite non-negative bit pattern b (and its negative) against b + 1;
+// 256 consecutive patterns per thread, the previous sigmoid carried.
+__global__ void __launch_bounds__(256) sigmoid_monotone_kernel(unsigned long long* bad) {
+  constexpr unsigned kPer = 256, kEnd = 0x7F800000u;  // +inf
+  const unsigned b0 = (blockIdx.x * 256u + threadIdx.x) * kPer;
+  if (b0 >= kEnd) return;
+  unsigned cnt = 0;
+  float pp = ycx_sigmoid(__uint_as_float(b0)), pn = ycx_sigmoid(__uint_as_float(b0 | 0x80000000u));
+  for (unsigned i = 1; i <= kPer && b0 + i <= kEnd; ++i) {
+    const unsigned b = b0 + i;
+    const float sp = ycx_sigmoid(__uint_as_float(b)), sn = ycx_sigmoid(__uint_as_float(b | 0x80000000u));
+    cnt += (sp < pp ? 1u : 0u) + (sn > pn ? 1u : 0u);  // +x rising, -x falling with b
+    pp = sp;
+    pn = sn;
+  }
+  if (cnt) atomicAdd(bad, (unsigned long long)cnt);
+}
+}  // namespace
+
+extern "C" ycx_status ycx_check_sigmoid_monotone(unsigned long long* violations, void* stream) {
+  YCX_CHECK_ARG(violations != nullptr);
+  const unsigned threads = 0x7F800000u / 256u;
+  hipLaunchKernelGGL(sigmoid_monotone_kernel, dim3((threads + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     violations);
+  return ycx_launch_status();
+}
 
 extern "C" ycx_status ycx_decode(const ycx_decode_desc* d, const float* head, float* out, void* stream) {
   YCX_CHECK_ARG(d && head && out);

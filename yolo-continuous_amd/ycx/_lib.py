@@ -134,6 +134,7 @@ _SIGS = [
     ("ycx_decode", _i32, [ctypes.POINTER(DecodeDesc), _VP, _VP, _VP]),
     ("ycx_filter_decoded", _i32, [ctypes.POINTER(FilterDesc), _VP, _VP, _VP, _VP, _VP]),
     ("ycx_decode_filter", _i32, [ctypes.POINTER(DecodeFilterDesc), ctypes.POINTER(_VP), _VP, _VP, _VP, _VP]),
+    ("ycx_check_sigmoid_monotone", _i32, [_VP, _VP]),
     ("ycx_nms_workspace_size", ctypes.c_size_t, [ctypes.POINTER(NmsDesc)]),
     ("ycx_sort_nms", _i32, [ctypes.POINTER(NmsDesc), _VP, _VP, _VP, _VP, ctypes.c_size_t, _VP, _VP, _VP, _VP]),
     ("ycx_run_ops", _i32, [ctypes.POINTER(Op), _i32, _VP, ctypes.POINTER(_VP)]),
