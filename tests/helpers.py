@@ -35,6 +35,14 @@ def make_model(cfg, nc, w_seed, precision='bf16'):
     return m, sd
 
 
+def make_model_cfg(cfg, nc, w_seed, precision='bf16'):
+    """make_model for a config dict (e.g. a built-in network with its head swapped)."""
+    m = Model(cfg, ANCHORS, nc, precision=precision).eval()
+    sd = synthetic_state_dict(m, seed=w_seed)
+    m.load_state_dict(sd)
+    return m, sd
+
+
 def g1_case(manifest, name, precision='bf16'):
     e = manifest['g1'][name]
     m, sd = make_model(e['cfg'], e['nc'], e['w_seed'], precision)
@@ -55,7 +63,7 @@ def rel_err(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
-def fused_keep_report(cand, cand_rows, counts, keep, kc, b, heads_b, nc, conf, iou, size, max_det):
+def fused_keep_report(cand, cand_rows, counts, keep, kc, b, heads_b, nc, conf, iou, size, max_det, mask=None):
     """Decompose the fused device path's result for image ``b`` against the
     oracle chain run on the SAME head logits (``heads_b``: CPU fp32 NCHW maps of
     that image, Detect order), so every difference is attributed:
@@ -72,7 +80,7 @@ def fused_keep_report(cand, cand_rows, counts, keep, kc, b, heads_b, nc, conf, i
     Returns a dict; tests print it and assert on each part."""
     from oracle import ref_post
     A = np.asarray(ANCHORS).reshape(-1, 2)
-    dec = torch.cat(ref_post.decode_box([h.unsqueeze(0) if h.dim() == 3 else h for h in heads_b], A, MASK, nc,
+    dec = torch.cat(ref_post.decode_box([h.unsqueeze(0) if h.dim() == 3 else h for h in heads_b], A, mask or MASK, nc,
                                         (size, size)), 1)
     ref_rows, _ = ref_post.nms_keep_rows(dec.clone(), nc, conf, iou)
     ref_rows = ref_rows[0].numpy()

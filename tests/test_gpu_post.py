@@ -309,6 +309,46 @@ def test_head_decode_fused_in_conv(device, cfg, nc, shape):
 
 
 @pytest.mark.parametrize('precision', ['f32', 'bf16'])
+def test_detector_idetect_model(device, precision):
+    """The fused Detector on an IDetect-headed network (yolov7-tiny with its head
+    swapped for IDetect, nets/idetect.py:7-50; ImplicitA/M folded into the head
+    convs): the head convs decode in their epilogue (bf16) or through
+    ycx_decode_filter (f32), then NMS; vs the oracle chain (decode_box -> nms,
+    detect.py:29-144) on the same GPU heads. IDetect's outputs are [P3, P4, P5]
+    with anchor rows 0, 1, 2, hence the mask."""
+    import copy
+    from helpers import make_model_cfg
+    cfg = copy.deepcopy(cvt_cfg('yolov7-tiny'))
+    assert cfg['head'][-1][2] == 'Detect'
+    cfg['head'][-1][2] = 'IDetect'
+    m, sd = make_model_cfg(cfg, 1, 0, precision)
+    m.to(device)
+    imask = [[0, 1, 2], [3, 4, 5], [6, 7, 8]]
+    shape = (2, 3, 320, 320)
+    det = Detector(m, shape, device, ANCHORS, imask, conf_thres=0.3, nms_thres=0.45, max_det=1000)
+    assert det.fused == (precision == 'bf16')
+    x = synthetic_images(*shape, seed=19).to(device)
+    dets, keep, kc = det(x)
+    torch.cuda.synchronize()
+    heads = [h.cpu() for h in det.heads]
+    assert [h.shape[2] for h in heads] == [40, 20, 10]
+    # the head maps are the network's own (oracle forward of the same weights, raw IDetect x_i)
+    ref = ref_forward.build(cfg, ANCHORS, 1, sd)(x.cpu())
+    ref = ref[1] if isinstance(ref, tuple) else ref
+    for h, r in zip(heads, ref):
+        r = r if r.dim() == 4 else r.permute(0, 1, 4, 2, 3).reshape(h.shape)
+        assert rel_err(h, r) < (1e-3 if precision == 'f32' else 5e-2)
+    cpu = [t.cpu() for t in (det.cand, det.cand_rows, det.counts, keep, kc)]
+    for b in range(2):
+        rep = fused_keep_report(*cpu, b, [h[b] for h in heads], 1, 0.3, 0.45, 320, 1000, mask=imask)
+        print(f"\n{precision} image {b}: {rep}")
+        assert rep['cls_same'] and rep['nms_exact'], rep
+        assert rep['box_maxdiff'] <= 2e-6 and rep['member_max_dist'] <= 1e-6, rep
+        assert rep['keep_flips'] <= FLIPS_PIN['tiny320'] and rep['unexplained_flips'] == 0, rep
+        assert int(kc[b]) > 0
+
+
+@pytest.mark.parametrize('precision', ['f32', 'bf16'])
 def test_detector_fused_path(device, precision):
     """Fused decode+filter+sort+NMS from the model's own heads vs the oracle
     chain (decode_box -> nms) run on the same GPU heads."""
