@@ -267,6 +267,12 @@ def lower_module(g: Graph, m, x):
     raise NotImplementedError(f"ycx: no HIP lowering for {type(m).__name__}")
 
 
+# Development A/B of tile choices: YCX_TILE_MAP="16:24/26,18:26" replaces the picked
+# tile 16 by 24 where cout_pad allows, else 26 (never set in the product path).
+_TILE_MAP = {int(a): [int(t) for t in b.split('/')] for a, b in
+             (kv.split(':') for kv in os.environ.get('YCX_TILE_MAP', '').split(',') if kv)}
+
+
 class Plan:
     """Device-independent lowering of a Model for one input shape: the graph
     after all passes, its outputs and its algorithmic FLOPs."""
@@ -661,6 +667,11 @@ class Engine:
         op.out = self._val_ptr(out, idx, 'out')
         op.residual = r.buf.tensor.data_ptr() if r is not None else None
         tile = 0 if stem else int(L.lib.ycx_conv_pick_tile(ctypes.byref(d)))
+        if not stem and tile in _TILE_MAP:  # development A/B only (YCX_TILE_MAP)
+            for t in _TILE_MAP[tile]:
+                if t not in (24, 25) or d.cout_pad % 256 == 0:
+                    tile = d.tile = t
+                    break
         name = 'stem' if stem else L.lib.ycx_conv_tile_name(tile).decode()
         self.op_info.append(dict(kind=node.kind, name=name, flops=flops, shape=shape, parts=node.p.get('parts', 1)))
         return op
