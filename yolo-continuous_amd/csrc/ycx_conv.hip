@@ -339,16 +339,27 @@ __device__ __forceinline__ void epilogue_regs(const ConvArgs& a, const f32x4 (&a
   }
 }
 
+// bias8_prefetch loads the bias of these channels (bias is [cout_pad]: always in bounds)
+// before the K loop, so the epilogue does not wait on a load round trip per fragment pair.
+template <int FM>
+__device__ __forceinline__ void bias8_prefetch(const ConvArgs& a, int cob, int lane, f32x4 (&bp)[FM]) {
+#pragma unroll
+  for (int k = 0; k < FM / 2; ++k) {
+    const int co = cob + 32 * k + 8 * (lane >> 4);
+    bp[2 * k] = *reinterpret_cast<const f32x4*>(a.bias + co);
+    bp[2 * k + 1] = *reinterpret_cast<const f32x4*>(a.bias + co + 4);
+  }
+}
+
 // epilogue_regs8 for fragments whose 16 pixels start at arbitrary pixel indices pxf[j].
 template <int FM, int FN>
 __device__ __forceinline__ void epilogue_frag8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob,
-                                               const int (&pxf)[FN], int lane) {
+                                               const int (&pxf)[FN], int lane, const f32x4 (&bp)[FM]) {
 #pragma unroll
   for (int k = 0; k < FM / 2; ++k) {
     const int co = cob + 32 * k + 8 * (lane >> 4);
     if (co >= a.Cout) continue;
-    const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + co);
-    const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bias + co + 4);
+    const f32x4 b0 = bp[2 * k], b1 = bp[2 * k + 1];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       float v[8];
@@ -365,17 +376,6 @@ __device__ __forceinline__ void epilogue_frag8(const ConvArgs& a, const f32x4 (&
 // NHWC epilogue for permuted A rows (conv_bf16_glds): fragments 2k, 2k+1 hold channels
 // cob + 32k + 8g .. +7 in C rows 4g..4g+3 (g = lane >> 4): one 16-byte store per lane and pixel
 // (store8: residual and x2 upsample included).
-// bias8_prefetch loads the bias of these channels (bias is [cout_pad]: always in bounds)
-// before the K loop, so the epilogue does not wait on a load round trip per fragment pair.
-template <int FM>
-__device__ __forceinline__ void bias8_prefetch(const ConvArgs& a, int cob, int lane, f32x4 (&bp)[FM]) {
-#pragma unroll
-  for (int k = 0; k < FM / 2; ++k) {
-    const int co = cob + 32 * k + 8 * (lane >> 4);
-    bp[2 * k] = *reinterpret_cast<const f32x4*>(a.bias + co);
-    bp[2 * k + 1] = *reinterpret_cast<const f32x4*>(a.bias + co + 4);
-  }
-}
 
 template <int FM, int FN>
 __device__ __forceinline__ void epilogue_regs8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob, int pxb,
@@ -1662,7 +1662,11 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3x3_halo(ConvArgs a) {
   int pxf[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) pxf[j] = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0;
-  if constexpr (FM % 2 == 0) epilogue_frag8<FM, FN>(a, acc, co0 + wm * TM, pxf, lane);
+  if constexpr (FM % 2 == 0) {
+    f32x4 bpre[FM];  // loaded here: prefetched before the K loop it cost this kernel 8-15 %
+    bias8_prefetch<FM>(a, co0 + wm * TM, lane, bpre);
+    epilogue_frag8<FM, FN>(a, acc, co0 + wm * TM, pxf, lane, bpre);
+  }
   else epilogue_frag<FM, FN>(a, acc, co0 + wm * TM, pxf, lane);
 }
 

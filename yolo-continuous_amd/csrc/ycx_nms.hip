@@ -625,11 +625,26 @@ __device__ void resolve(const Ctx<kLds>& c, const Frame& fr, const Ptrs& P, unsi
       if (st[r] != 0) continue;
       const int ns = P.nsup[off + p];
       int res = 0;  // 0: every suppressor removed, 1: some undecided, 2: one kept
-      const int* sl = P.slots + (size_t)(off + p) * kSlots;
-      for (int k = 0; k < min(ns, kSlots); ++k) {
-        const unsigned char sj = st[sl[k]];
-        if (sj == 1) { res = 2; break; }
-        if (sj == 0) res = 1;
+      // the box's cached suppressors in one 64-byte read (one memory round trip per box
+      // and round instead of one per suppressor); entries past ns are never looked at
+      const int4* sl4 = reinterpret_cast<const int4*>(P.slots + (size_t)(off + p) * kSlots);
+      int sl[kSlots];
+#pragma unroll
+      for (int q = 0; q < kSlots / 4; ++q) {
+        const int4 v = sl4[q];
+        sl[4 * q] = v.x;
+        sl[4 * q + 1] = v.y;
+        sl[4 * q + 2] = v.z;
+        sl[4 * q + 3] = v.w;
+      }
+      const int nc_ = min(ns, kSlots);
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) {
+        if (k < nc_ && res != 2) {
+          const unsigned char sj = st[sl[k]];
+          if (sj == 1) res = 2;
+          else if (sj == 0) res = 1;
+        }
       }
       if (ns > kSlots && res == 0) {  // the cached ones are all removed: look at the rest
         const f32x4 b = c.sbox[p];
