@@ -804,6 +804,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     }
     __builtin_amdgcn_sched_barrier(0);
     STAMP(4);
+#ifdef YCX_GLDS_SETPRIO  // development A/B: MFMA phase at raised wave priority
+    __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk)
 #pragma unroll
@@ -811,6 +814,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+#ifdef YCX_GLDS_SETPRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     STAMP(5);
 #ifdef YCX_GLDS_STAMP
@@ -2989,7 +2995,11 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
     case 13: return launch_glds<64, 256, 1, 8, true>(a, st);
     case 14: return launch_glds<128, 256, 2, 4, true>(a, st);
     case 15: return launch_glds<64, 256, 1, 8, false, 2>(a, st);
+#ifdef YCX_T16_NSB3  // development A/B: activation ring one K step deeper
+    case 16: return launch_glds<128, 128, 2, 4, false, 2, 3>(a, st);
+#else
     case 16: return launch_glds<128, 128, 2, 4, false, 2>(a, st);
+#endif
     case 17: return launch_glds<64, 256, 1, 8, true, 2>(a, st);
     case 18: return launch_glds<64, 128, 1, 8, false, 2>(a, st);
     case 19: return launch_halo<64, 1, 4, 3>(a, st);
