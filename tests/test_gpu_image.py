@@ -8,6 +8,7 @@ import yaml
 
 from helpers import ANCHORS, MASK
 from oracle import ref_letterbox
+from ycx.utils.target_box import TargetBox
 from ycx.detect import correct_boxes_device, predict, yolo_correct_boxes
 from ycx.utils.letterbox import letterbox_geometry, letterbox_gpu
 
@@ -67,5 +68,42 @@ def test_predict_headless(device, tmp_path):
                     nms_threshold=0.3)
     assert isinstance(boxes, list)
     for b in boxes:  # detect.py:236-244 clamps each corner on one side only, like the reference
-        x1, y1, x2, y2 = b['box']
-        assert x1 >= 0 and y1 >= 0 and x2 <= 773 and y2 <= 512 and b['label'] == 'raccoon'
+        x1, y1, x2, y2 = b.left, b.top, b.right, b.bottom
+        assert x1 >= 0 and y1 >= 0 and x2 <= 773 and y2 <= 512 and b.label == 'raccoon'
+    assert all(isinstance(b, TargetBox) for b in boxes)
+
+
+def test_predict_vs_oracle_chain(device, tmp_path):
+    """predict (detect.py:208-265) against the oracle chain on the same image: the
+    letterbox restatement (oracle/ref_letterbox.py), the fp32 forward
+    (oracle/ref_forward.py), decode_box + non_max_suppression + yolo_correct_boxes
+    (oracle/ref_post.py), then detect.py:236-244's floor/clamp. f32 parity mode
+    (1e-3): the same boxes in the same order, corners within one pixel (a
+    floor can cross an integer), scores within 1e-3, same labels."""
+    from oracle import ref_forward, ref_letterbox, ref_post
+    from ycx.utils.helper_io import cvt_cfg
+    from ycx.utils.synth import synthetic_state_dict
+    plan = dict(device=0, image_size=320, image_chan=3, labels=['raccoon'], model_cfg='yolov7-tiny',
+                anchors=ANCHORS, anchors_mask=MASK)
+    cfg = tmp_path / 'plan.yaml'
+    cfg.write_text(yaml.safe_dump(plan))
+    img = np.random.default_rng(4).integers(0, 256, size=(287, 411, 3), dtype=np.uint8)
+    got = predict(str(cfg), image=img, weights='synthetic', device='cuda:0', conf_threshold=0.3,
+                  nms_threshold=0.3, precision='f32')
+    net_cfg = cvt_cfg('yolov7-tiny')
+    from ycx.nets.yolo import Model
+    sd = synthetic_state_dict(Model(net_cfg, ANCHORS, 1), seed=0)
+    x = torch.from_numpy(ref_letterbox.letterbox_tensor(img, (320, 320))).unsqueeze(0)
+    heads = ref_forward.build(net_cfg, ANCHORS, 1, sd)(x)
+    A = np.asarray(ANCHORS).reshape(-1, 2)
+    dec = torch.cat(ref_post.decode_box(heads, A, MASK, 1, (320, 320)), 1)
+    res = ref_post.non_max_suppression(dec, 1, (320, 320), np.array(img.shape[0:2]), True, 0.3, 0.3)[0]
+    assert res is not None and len(got) == len(res) > 0, (len(got), None if res is None else len(res))
+    for tb, row in zip(got, res):
+        y1, x1, y2, x2 = row[0], row[1], row[2], row[3]
+        want = [max(0, int(np.floor(x1))), max(0, int(np.floor(y1))),
+                min(img.shape[1], int(np.floor(x2))), min(img.shape[0], int(np.floor(y2)))]
+        assert max(abs(a - b) for a, b in zip([tb.left, tb.top, tb.right, tb.bottom], want)) <= 1
+        assert abs(float(tb.score) - float(row[4] * row[5])) <= 1e-3
+        assert tb.label == 'raccoon' and tb.color == (255, 0, 0)
+

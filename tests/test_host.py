@@ -21,3 +21,17 @@ def test_yolo_correct_boxes_matches_oracle(letterbox, image_hw):
     assert got.dtype == want.dtype and got.shape == want.shape == (257, 4)
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(wh_a, wh_b)  # the same in-place side effect on the caller's array
+
+
+def test_target_box_record():
+    """utils/target_box.py:8-38 API: corner fields, accessors, printable record;
+    the palette of utils/helper_cv.py:60-64."""
+    from ycx.utils.target_box import TargetBox, colors_for
+    tb = TargetBox([3, 4, 50, 60], 0.75, 'dog', (255, 0, 0))
+    assert (tb.left, tb.top, tb.right, tb.bottom) == (3, 4, 50, 60)
+    assert tb.get_topleft() == (3, 4) and tb.get_bottomright() == (50, 60)
+    text = str(tb)
+    assert text.startswith('-' * 20 + 'TargetBox') and 'dog' in text and '0.75' in text
+    assert colors_for(3) == [(255, 0, 0), (0, 255, 0), (0, 0, 255)]
+    assert colors_for(1) == [(255, 0, 0)]
+

@@ -804,7 +804,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     }
     __builtin_amdgcn_sched_barrier(0);
     STAMP(4);
-#ifdef YCX_GLDS_SETPRIO  // development A/B: MFMA phase at raised wave priority
+#ifndef YCX_GLDS_NO_SETPRIO  // MFMA phase at raised wave priority (concurrent bench +0.6-1.2 %)
     __builtin_amdgcn_s_setprio(1);
 #endif
 #pragma unroll
@@ -814,7 +814,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
-#ifdef YCX_GLDS_SETPRIO
+#ifndef YCX_GLDS_NO_SETPRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
     __builtin_amdgcn_sched_barrier(0);

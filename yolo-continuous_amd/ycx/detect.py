@@ -465,19 +465,24 @@ def prepare_model(plan, weights=None, device=None, precision='bf16'):
 
 
 def predict(cfg_file, image_path=None, conf_threshold=0.3, nms_threshold=0.3, *, image=None, device=None,
-            weights=None, show=False):
+            weights=None, show=False, precision='bf16'):
     """detect.py:208-265, headless by default. ``image`` may be an HWC uint8 BGR
-    array instead of a path. Returns the list of TargetBox-like dicts it prints."""
+    array instead of a path. Returns (and prints) the reference's TargetBox
+    records (utils/target_box.py): corners floored and clamped to the image as
+    detect.py:236-244 does, score obj * cls_conf, the plan's label name and its
+    palette colour (utils/helper_cv.py:60-64)."""
     from .cfg.train_plan import TrainPlan
     from .utils.helper_io import check_file
     from .utils.helper_torch import select_device
     from .utils.letterbox import letterbox_gpu, read_image
+    from .utils.target_box import TargetBox, colors_for
     plan = TrainPlan(check_file(cfg_file))
     dev = select_device(device if device is not None else plan.device)
     target = (plan.image_size, plan.image_size)
     anchors = np.asarray(plan.anchors).reshape(-1, 2)
+    colors = colors_for(plan.num_labels)
     original = image if image is not None else read_image(image_path)
-    net = prepare_model(plan, weights=weights, device=dev)
+    net = prepare_model(plan, weights=weights, device=dev, precision=precision)
     images = letterbox_gpu(original, target, device=dev).unsqueeze(0)  # detect.py:23-26 on the GPU
     with torch.no_grad():
         pred = net(images)
@@ -487,12 +492,12 @@ def predict(cfg_file, image_path=None, conf_threshold=0.3, nms_threshold=0.3, *,
                                   conf_thres=conf_threshold, nms_thres=nms_threshold)
     boxes = []
     if results[0] is not None:
-        r = results[0]
-        for row in r:
+        for row in results[0]:  # rows are (y1, x1, y2, x2, obj, cls_conf, cls) after yolo_correct_boxes
             y1, x1, y2, x2 = row[0], row[1], row[2], row[3]
             box = [max(0, int(np.floor(x1))), max(0, int(np.floor(y1))),
                    min(original.shape[1], int(np.floor(x2))), min(original.shape[0], int(np.floor(y2)))]
             label = int(row[6])
-            boxes.append(dict(box=box, score=float(row[4] * row[5]), label=plan.labels[label]))
-            print(f"{plan.labels[label]}\t{row[4] * row[5]:.3f}\t{box}")
+            tb = TargetBox(box, row[4] * row[5], plan.labels[label], colors[label])
+            print(tb)
+            boxes.append(tb)
     return boxes
