@@ -305,6 +305,9 @@ __device__ __forceinline__ void epilogue_regs(const ConvArgs& a, const f32x4 (&a
                                               int lane) {
   if (a.out_layout == YCX_OUT_NCHW_F32) {
     float* Y = reinterpret_cast<float*>(a.y);
+    f32x4 bb[FM];  // all bias loads first (bias is [cout_pad]): one round trip, not one per element
+#pragma unroll
+    for (int i = 0; i < FM; ++i) bb[i] = *reinterpret_cast<const f32x4*>(a.bias + cob + i * 16 + (lane >> 4) * 4);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -317,7 +320,7 @@ __device__ __forceinline__ void epilogue_regs(const ConvArgs& a, const f32x4 (&a
           int co = cob + i * 16 + (lane >> 4) * 4 + r;
           if (co < a.Cout)
             Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] =
-                ycx_act<true>(acc[i][j][r] + a.bias[co], a.act, a.slope);
+                ycx_act<true>(acc[i][j][r] + bb[i][r], a.act, a.slope);
         }
       }
     return;
@@ -974,12 +977,21 @@ template <int FM, int FN>
 __device__ __forceinline__ void epilogue_f8x8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob, int pxb,
                                               int lane) {
   const float* dq = a.bias + a.Cout_pad;
+  // every bias / dq vector first (bias is [2 cout_pad]: in bounds), one load round trip in all
+  f32x4 bb[FM], qq[FM];
+#pragma unroll
+  for (int k = 0; k < FM / 2; ++k) {
+    const int co = cob + 32 * k + 8 * (lane >> 4);
+    bb[2 * k] = *reinterpret_cast<const f32x4*>(a.bias + co);
+    bb[2 * k + 1] = *reinterpret_cast<const f32x4*>(a.bias + co + 4);
+    qq[2 * k] = *reinterpret_cast<const f32x4*>(dq + co);
+    qq[2 * k + 1] = *reinterpret_cast<const f32x4*>(dq + co + 4);
+  }
 #pragma unroll
   for (int k = 0; k < FM / 2; ++k) {
     const int co = cob + 32 * k + 8 * (lane >> 4);
     if (co >= a.Cout) continue;  // cout % 8 == 0
-    const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + co), b1 = *reinterpret_cast<const f32x4*>(a.bias + co + 4);
-    const f32x4 q0 = *reinterpret_cast<const f32x4*>(dq + co), q1 = *reinterpret_cast<const f32x4*>(dq + co + 4);
+    const f32x4 b0 = bb[2 * k], b1 = bb[2 * k + 1], q0 = qq[2 * k], q1 = qq[2 * k + 1];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int p = pxb + j * 16 + (lane & 15);
@@ -1001,6 +1013,13 @@ __device__ __forceinline__ void epilogue_f8(const ConvArgs& a, const f32x4 (&acc
   const float* dq = a.bias + a.Cout_pad;
   if (a.out_layout == YCX_OUT_NCHW_F32) {
     float* Y = reinterpret_cast<float*>(a.y);
+    f32x4 bb[FM], qq[FM];  // all loads first (bias is [2 cout_pad]): one round trip, not one per element
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int co = cob + i * 16 + (lane >> 4) * 4;
+      bb[i] = *reinterpret_cast<const f32x4*>(a.bias + co);
+      qq[i] = *reinterpret_cast<const f32x4*>(dq + co);
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -1013,7 +1032,7 @@ __device__ __forceinline__ void epilogue_f8(const ConvArgs& a, const f32x4 (&acc
           const int co = cob + i * 16 + (lane >> 4) * 4 + r;
           if (co < a.Cout)
             Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] =
-                ycx_act<true>(fmaf(acc[i][j][r], dq[co], a.bias[co]), a.act, a.slope);
+                ycx_act<true>(fmaf(acc[i][j][r], qq[i][r], bb[i][r]), a.act, a.slope);
         }
       }
     return;
