@@ -39,10 +39,22 @@
 namespace {
 
 constexpr int kThreads = 1024;
+// nms_big's workgroup, LDS budget and grid (build-time knobs, DESIGN.md §6 tried-and-rejected)
+#ifndef YCX_NMS_BIG_THREADS
+#define YCX_NMS_BIG_THREADS 1024
+#endif
+#ifndef YCX_NMS_BIG_LDS
+#define YCX_NMS_BIG_LDS 159744
+#endif
+constexpr int kBigThreads = YCX_NMS_BIG_THREADS;
+constexpr int kBigLds = YCX_NMS_BIG_LDS;
 constexpr int kMaxNc = 1024;      // classes handled in LDS
 constexpr int kRegMax = 512;      // largest class finished in registers (R = 8 slots per lane)
 constexpr int kMaxRows = 131072;  // rows (candidates) per image
-constexpr int kBigBlocks = 256;   // nms_big grid (task-strided)
+#ifndef YCX_NMS_BIG_BLOCKS
+#define YCX_NMS_BIG_BLOCKS 256
+#endif
+constexpr int kBigBlocks = YCX_NMS_BIG_BLOCKS;   // nms_big grid (task-strided)
 constexpr int kSlots = 16;        // highest-ranked suppressors cached per box
 constexpr int kLevels = 7;        // size octaves: level L holds max(w, h) < 2^-L of the class extent
 constexpr int kGridCells = 5461;  // sum_{L < 7} 4^L
@@ -330,7 +342,7 @@ __device__ void sort_class(const ycx_cand* __restrict__ ci, const int* bucket, i
     const int e = threadIdx.x * E + i;
     v[i] = e < S ? make_key(ci[bucket[e]]) : ~0ull;
   }
-  sort_regs<E>(v, lds, E * kThreads);
+  sort_regs<E>(v, lds, E * (int)blockDim.x);
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < E; ++i) lds[threadIdx.x * E + i] = v[i];
@@ -553,7 +565,7 @@ __device__ void resolve(const Ctx<kLds>& c, const Frame& fr, const Ptrs& P, unsi
   // neighbourhood). Each box keeps its kSlots highest-ranked suppressors
   // (smallest ranks, ascending): they decide most boxes, and a box needs a
   // rescan only when all of them end up removed while more exist.
-  for (int p = tid; p < S; p += kThreads) {
+  for (int p = tid; p < S; p += kBigThreads) {
     const int r = c.rank(p);
     const f32x4 b = c.sbox[p];
     const float a = box_area(b);
@@ -613,14 +625,14 @@ __device__ void resolve(const Ctx<kLds>& c, const Frame& fr, const Ptrs& P, unsi
 #endif
   }
   // (5) greedy as a fixed point over ranks: 0 undecided, 1 kept, 2 removed
-  for (int r = tid; r < S; r += kThreads) st[r] = 0;
+  for (int r = tid; r < S; r += kBigThreads) st[r] = 0;
   __syncthreads();
   YCX_PROF_MARK(2)
   for (int it = 0; it <= S; ++it) {  // every round decides at least one box
     if (tid == 0) *s_flag = 0;
     __syncthreads();
     int undecided = 0;
-    for (int p = tid; p < S; p += kThreads) {
+    for (int p = tid; p < S; p += kBigThreads) {
       const int r = c.rank(p);
       if (st[r] != 0) continue;
       const int ns = P.nsup[off + p];
@@ -690,7 +702,7 @@ __device__ __forceinline__ int block_exclusive(int v, int* s_w, int* total) {
   if (lane == 63) s_w[wid] = incl;
   __syncthreads();
   int pre = 0, tot = 0;
-  for (int w = 0; w < kThreads / 64; ++w) {
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
     const int x = s_w[w];
     pre += w < wid ? x : 0;
     tot += x;
@@ -701,15 +713,15 @@ __device__ __forceinline__ int block_exclusive(int v, int* s_w, int* total) {
 }
 
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) nms_big(ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws,
+__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_big(ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws,
                                                     Thr thr, float t_lo, float inv_t, int all_pairs) {
-  constexpr int kLdsBytes = 159744;
+  constexpr int kLdsBytes = kBigLds;
   constexpr int kLdsCellBytes = ((kCells * 4) + 255) & ~255;
-  static_assert(kLdsBytes >= 16384 * 8, "LDS keys");
+  static_assert(kLdsBytes >= 16 * kBigThreads * 8, "LDS keys of the register sorts (E <= 16)");
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
   __shared__ int s_lv[kLevels][5];
   __shared__ int s_ext[4];
-  __shared__ int s_w[kThreads / 64];
+  __shared__ int s_w[kBigThreads / 64];
   __shared__ int s_flag;
   const int tid = threadIdx.x;
   const int rows = d.rows_total;
@@ -738,23 +750,23 @@ __global__ void __launch_bounds__(kThreads) nms_big(ycx_nms_desc d, const ycx_ca
       s_lv[tid][3] = s_lv[tid][4] = 0x7F800000;  // +inf
     }
     // (1) rank = position in (score desc, row asc) order
-    const int Pn = max(next_pow2(S), kThreads);
+    const int Pn = max(next_pow2(S), kBigThreads);
     unsigned long long* keys =
         Pn <= kLdsBytes / 8 ? reinterpret_cast<unsigned long long*>(smem) : P.keys + 2 * (size_t)off;
-    switch (Pn / kThreads) {  // uniform
+    switch (Pn / kBigThreads) {  // uniform
       case 1: sort_class<1>(ci, bucket, S, keys); break;
       case 2: sort_class<2>(ci, bucket, S, keys); break;
       case 4: sort_class<4>(ci, bucket, S, keys); break;
       case 8: sort_class<8>(ci, bucket, S, keys); break;
       case 16: sort_class<16>(ci, bucket, S, keys); break;
       default:  // > 16384 keys: workspace bitonic
-        for (int i = tid; i < Pn; i += kThreads) keys[i] = i < S ? make_key(ci[bucket[i]]) : ~0ull;
+        for (int i = tid; i < Pn; i += kBigThreads) keys[i] = i < S ? make_key(ci[bucket[i]]) : ~0ull;
         __syncthreads();
         block_bitonic(keys, Pn);
     }
     YCX_PROF_MARK(0)
     // (2) bucket in rank order; extent of the class's regular boxes
-    for (int r = tid; r < S; r += kThreads) {
+    for (int r = tid; r < S; r += kBigThreads) {
       const int row = (int)(unsigned)keys[r];
       bucket[r] = row;
       const ycx_cand b = ci[row];
@@ -766,20 +778,20 @@ __global__ void __launch_bounds__(kThreads) nms_big(ycx_nms_desc d, const ycx_ca
       }
     }
     __syncthreads();  // keys dead from here: LDS becomes the cell table
-    for (int k = tid; k < kCells; k += kThreads) cells[k] = 0;
+    for (int k = tid; k < kCells; k += kBigThreads) cells[k] = 0;
     __syncthreads();
     const float X0 = o2f(s_ext[0]), Y0 = o2f(s_ext[1]);
     const float E = fmaxf(o2f(s_ext[2]) - X0, o2f(s_ext[3]) - Y0);
     const float inv = (E > 0.0f && E < INFINITY) ? 1.0f / E : 0.0f;  // 0: every box irregular
     // (3) spatial counting sort: histogram (cell id parked in nsup[rank]), scan, scatter
-    for (int r = tid; r < S; r += kThreads) {
+    for (int r = tid; r < S; r += kBigThreads) {
       const ycx_cand b = ci[bucket[r]];
       const Geo g = geometry(f32x4{b.x1, b.y1, b.x2, b.y2}, X0, Y0, inv, all_pairs);
       P.nsup[off + r] = g.cell;
       atomicAdd(&cells[g.cell], 1);
     }
     // per-level count / extreme sizes: reduced per wave, one LDS atomic per wave and level
-    for (int r0 = 0; r0 < S; r0 += kThreads) {  // uniform trip count
+    for (int r0 = 0; r0 < S; r0 += kBigThreads) {  // uniform trip count
       const int r = r0 + tid;
       Geo g;
       g.level = -1;
@@ -820,7 +832,7 @@ __global__ void __launch_bounds__(kThreads) nms_big(ycx_nms_desc d, const ycx_ca
     unsigned char* st = lds ? reinterpret_cast<unsigned char*>(smem + kLdsCellBytes + 16 * S + ((2 * S + 15) & ~15))
                             : S <= kLdsBytes - kLdsCellBytes ? reinterpret_cast<unsigned char*>(smem + kLdsCellBytes)
                                                              : P.state + off;
-    for (int r = tid; r < S; r += kThreads) {
+    for (int r = tid; r < S; r += kBigThreads) {
       const int q = atomicAdd(&cells[P.nsup[off + r]], 1);  // cells[k] ends as the end of cell k
       const ycx_cand b = ci[bucket[r]];
       if (lds) {
@@ -846,7 +858,7 @@ __global__ void __launch_bounds__(kThreads) nms_big(ycx_nms_desc d, const ycx_ca
 #endif
     // (6) kept rows in rank order
     int base = 0;
-    for (int r0 = 0; r0 < S; r0 += kThreads) {
+    for (int r0 = 0; r0 < S; r0 += kBigThreads) {
       const int r = r0 + tid;
       const int k = (r < S && st[r] == 1) ? 1 : 0;
       int total;
@@ -953,7 +965,7 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   const float t_lo = all_pairs ? 0.0f : (float)(fmin(d->iou_thres, 1.0) * (1.0 - 1e-3));
   const float inv_t = t_lo > 0.0f ? 1.0f / t_lo : INFINITY;
   hipLaunchKernelGGL(nms_prep, dim3(d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws, t);
-  hipLaunchKernelGGL(nms_big, dim3(kBigBlocks), dim3(kThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
+  hipLaunchKernelGGL(nms_big, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
   hipLaunchKernelGGL(nms_finish, dim3(d->n), dim3(kThreads), 0, st, *d, cand, ws, dets, keep_rows, keep_counts);
   return ycx_launch_status();
 }
