@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define YCX_ABI_VERSION 4
+#define YCX_ABI_VERSION 5
 
 typedef int32_t ycx_status;
 enum {
@@ -96,6 +96,10 @@ typedef struct ycx_pool_desc {
   int32_t ho, wo, out_c_off, out_c_stride;
   int32_t k, stride, pad;
   int32_t dtype;
+  /* levels > 1: a cascade of `levels` identical 'same' pools (stride 1, pad k/2) in one
+   * launch, pool i of pool i-1 (SPPCSPC's 5/9/13 as 5, 5o5, 5o5o5: nets/common.py:257),
+   * level i written to channels out_c_off + i*c of y. 0 or 1: one pool. */
+  int32_t levels;
 } ycx_pool_desc;
 
 /* Channel-slice copy with optional nearest x2 upsample (scale = 1 or 2).

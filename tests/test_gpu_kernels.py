@@ -189,6 +189,41 @@ def test_maxpool(device, dtype, k, s, p):
     assert torch.equal(yd.cpu()[..., 16:].float(), ref)  # max is exact
 
 
+@pytest.mark.parametrize('hw,c,k', [((20, 20), 512, 5), ((11, 13), 48, 5), ((40, 40), 256, 3), ((7, 9), 16, 7)])
+@pytest.mark.parametrize('fp8', [False, True])
+def test_maxpool_cascade(device, hw, c, k, fp8):
+    """levels = 3 (SPPCSPC's 5 / 9 / 13 as a k5 cascade, one launch, the plane in LDS) vs
+    torch max_pool2d applied level after level; level i lands at out_c_off + i*c. Max is exact:
+    bf16 bit for bit, e4m3 bytes bit for bit (values go through float and back unchanged)."""
+    n, (h, w) = 2, hw
+    g = torch.Generator().manual_seed(3)
+    xf = torch.randn(n, h, w, c + 16, generator=g) * 4
+    if fp8:
+        x = xf.to(torch.float8_e4m3fn)
+        xv, dt = x.float(), L.DT_FP8
+        y = torch.zeros(n, h, w, 3 * c + 32, dtype=torch.uint8)
+        xd = x.view(torch.uint8).to(device)
+    else:
+        x = xf.to(torch.bfloat16)
+        xv, dt = x.float(), L.DT_BF16
+        y = torch.zeros(n, h, w, 3 * c + 32, dtype=torch.bfloat16)
+        xd = x.to(device)
+    d = L.PoolDesc()
+    d.n, d.h, d.w, d.c, d.in_c_off, d.in_c_stride = n, h, w, c, 16, c + 16
+    d.ho, d.wo, d.out_c_off, d.out_c_stride = h, w, 32, 3 * c + 32
+    d.k, d.stride, d.pad, d.dtype, d.levels = k, 1, k // 2, dt, 3
+    yd = y.to(device)
+    L.check(L.lib.ycx_maxpool(ctypes.byref(d), xd.data_ptr(), yd.data_ptr(), L.stream_handle(device)))
+    got = yd.cpu()
+    cur = xv[..., 16:].permute(0, 3, 1, 2)
+    for lv in range(3):
+        cur = F.max_pool2d(cur, k, 1, k // 2)
+        sl = got[..., 32 + lv * c:32 + (lv + 1) * c]
+        sl = sl.view(torch.float8_e4m3fn).float() if fp8 else sl.float()
+        assert torch.equal(sl, cur.permute(0, 2, 3, 1)), lv
+    assert not got[..., :32].any()  # channels before out_c_off untouched
+
+
 @pytest.mark.parametrize('dtype', [L.DT_BF16, L.DT_F32])
 @pytest.mark.parametrize('scale,nchw', [(1, False), (2, False), (1, True)])
 def test_copy_upsample(device, dtype, scale, nchw):

@@ -179,6 +179,87 @@ __global__ void __launch_bounds__(256) quantize_f8_kernel(const float* __restric
   }
 }
 
+// Cascade of `levels` k x k 'same' max-pools (stride 1) in one launch: one workgroup per
+// (image, CC-channel slice) holds the whole H x W plane in LDS (raw elements), and each level
+// is a row pass then a column pass (a k x k max with -inf padding is separable); level i goes
+// to channels out_c_off + i*c. E = bytes per element (2 bf16, 1 e4m3); 16-byte chunks.
+template <int E>
+__device__ __forceinline__ void chunk_to_f(uint4 v, float (&f)[16 / E]) {
+  if constexpr (E == 2) {
+    const __bf16* b = reinterpret_cast<const __bf16*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (float)b[j];
+  } else {
+    float* g = f;
+    f8x8_unpack(make_uint2(v.x, v.y), g);
+    f8x8_unpack(make_uint2(v.z, v.w), g + 8);
+  }
+}
+template <int E>
+__device__ __forceinline__ uint4 f_to_chunk(const float (&f)[16 / E]) {
+  uint4 v;
+  if constexpr (E == 2) {
+    __bf16* b = reinterpret_cast<__bf16*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = (__bf16)f[j];  // exact: every value is an input element
+  } else {
+    v.x = f8x4_pack_sat(f[0], f[1], f[2], f[3]);
+    v.y = f8x4_pack_sat(f[4], f[5], f[6], f[7]);
+    v.z = f8x4_pack_sat(f[8], f[9], f[10], f[11]);
+    v.w = f8x4_pack_sat(f[12], f[13], f[14], f[15]);
+  }
+  return v;
+}
+
+template <int E>
+__global__ void __launch_bounds__(256) maxpool_cascade_kernel(ycx_pool_desc d, int cc, const uint8_t* __restrict__ x,
+                                                              uint8_t* __restrict__ y) {
+  extern __shared__ uint4 lds_chunks[];
+  constexpr int NE = 16 / E;
+  const int H = d.h, W = d.w, HW = H * W, r = d.k / 2;
+  const int nchunk = cc * E / 16;  // 16-byte chunks per pixel in this slice
+  const int items = HW * nchunk;
+  const int n = blockIdx.x / (d.c / cc), c0 = (blockIdx.x % (d.c / cc)) * cc;
+  uint4* S = lds_chunks;           // [HW][nchunk]: the level's source
+  uint4* T = lds_chunks + items;   // [HW][nchunk]: after the row pass
+  const size_t px0 = (size_t)n * HW;
+  for (int i = threadIdx.x; i < items; i += blockDim.x) {
+    const int pix = i / nchunk, g = i - pix * nchunk;
+    S[i] = *reinterpret_cast<const uint4*>(x + ((px0 + pix) * d.in_c_stride + d.in_c_off + c0) * E + g * 16);
+  }
+  __syncthreads();
+  for (int lv = 0; lv < d.levels; ++lv) {
+    for (int i = threadIdx.x; i < items; i += blockDim.x) {  // row pass
+      const int pix = i / nchunk, g = i - pix * nchunk, yy = pix / W, xx = pix - yy * W;
+      float m[NE], f[NE];
+#pragma unroll
+      for (int j = 0; j < NE; ++j) m[j] = -INFINITY;
+      for (int xi = max(xx - r, 0); xi <= min(xx + r, W - 1); ++xi) {
+        chunk_to_f<E>(S[(yy * W + xi) * nchunk + g], f);
+#pragma unroll
+        for (int j = 0; j < NE; ++j) m[j] = fmaxf(m[j], f[j]);
+      }
+      T[i] = f_to_chunk<E>(m);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < items; i += blockDim.x) {  // column pass: the level's output
+      const int pix = i / nchunk, g = i - pix * nchunk, yy = pix / W, xx = pix - yy * W;
+      float m[NE], f[NE];
+#pragma unroll
+      for (int j = 0; j < NE; ++j) m[j] = -INFINITY;
+      for (int yi = max(yy - r, 0); yi <= min(yy + r, H - 1); ++yi) {
+        chunk_to_f<E>(T[(yi * W + xx) * nchunk + g], f);
+#pragma unroll
+        for (int j = 0; j < NE; ++j) m[j] = fmaxf(m[j], f[j]);
+      }
+      const uint4 v = f_to_chunk<E>(m);
+      S[i] = v;  // the next level's source (every row pass read of S is behind the barrier above)
+      *reinterpret_cast<uint4*>(y + ((px0 + pix) * d.out_c_stride + d.out_c_off + lv * d.c + c0) * E + g * 16) = v;
+    }
+    __syncthreads();
+  }
+}
+
 unsigned grid_for(long long total) {
   long long b = (total + 255) / 256;
   if (b > 256LL * 16) b = 256LL * 16;  // grid-stride beyond 16 blocks per CU
@@ -199,6 +280,25 @@ extern "C" ycx_status ycx_maxpool(const ycx_pool_desc* d, const void* x, void* y
   YCX_CHECK_SUPPORTED(d->c % vn == 0 && d->in_c_off % vn == 0 && d->in_c_stride % vn == 0 &&
                       d->out_c_off % vn == 0 && d->out_c_stride % vn == 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (d->levels > 1) {
+    YCX_CHECK_ARG(d->stride == 1 && d->k % 2 == 1 && d->pad == d->k / 2 && d->ho == d->h && d->wo == d->w);
+    YCX_CHECK_ARG(d->out_c_off + d->levels * d->c <= d->out_c_stride);
+    YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_FP8);
+    const int esz = d->dtype == YCX_DT_BF16 ? 2 : 1;
+    // widest channel slice (16-byte multiple, dividing c) whose two planes fit 64 KB of LDS
+    const long long hw = (long long)d->h * d->w;
+    int cc = 0;
+    for (int t = 128; t * esz >= 16; t >>= 1)
+      if (d->c % t == 0 && 2 * hw * t * esz <= 65536) { cc = t; break; }
+    YCX_CHECK_SUPPORTED(cc > 0);
+    const dim3 g((unsigned)(d->n * (d->c / cc)));
+    const size_t lds = (size_t)(2 * hw * cc * esz);
+    if (esz == 2)
+      hipLaunchKernelGGL(maxpool_cascade_kernel<2>, g, dim3(256), lds, st, *d, cc, (const uint8_t*)x, (uint8_t*)y);
+    else
+      hipLaunchKernelGGL(maxpool_cascade_kernel<1>, g, dim3(256), lds, st, *d, cc, (const uint8_t*)x, (uint8_t*)y);
+    return ycx_launch_status();
+  }
   long long total = (long long)d->n * d->ho * d->wo * (d->c / vn);
   if (d->dtype == YCX_DT_FP8)
     hipLaunchKernelGGL(maxpool_f8_kernel, dim3(grid_for(total)), dim3(256), 0, st, *d, (const uint8_t*)x,

@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see above)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("YCX_LIB", os.path.join(_HERE, "libycx_hip.so"))
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # ---- enums (ycx.h) ----
 YCX_OK, YCX_ERR_BAD_ARG, YCX_ERR_UNSUPPORTED, YCX_ERR_LAUNCH, YCX_ERR_CAPACITY = 0, 1, 2, 3, 4
@@ -42,7 +42,7 @@ class ConvDesc(ctypes.Structure):
 class PoolDesc(ctypes.Structure):
     _fields_ = [(n, _i32) for n in (
         "n", "h", "w", "c", "in_c_off", "in_c_stride",
-        "ho", "wo", "out_c_off", "out_c_stride", "k", "stride", "pad", "dtype")]
+        "ho", "wo", "out_c_off", "out_c_stride", "k", "stride", "pad", "dtype", "levels")]
 
 
 class CopyDesc(ctypes.Structure):

@@ -552,6 +552,9 @@ class Engine:
             self.buffers.append(b.tensor)
         ops, self.input_slots, self.output_slots, self.op_info = [], [], {}, []
         self.conv_flops = 0
+        cascades = self._pool_cascades()
+        for c in cascades.values():
+            fused.update(id(nd) for nd in c[1:])
         for node in self.graph.nodes:
             k = node.kind
             if id(node) in fused:
@@ -561,7 +564,7 @@ class Engine:
             elif k in ('conv', 'stem'):
                 ops.append(self._conv_op(node))
             elif k == 'pool':
-                ops.append(self._pool_op(node))
+                ops.append(self._pool_op(node, levels=len(cascades.get(id(node), [node]))))
             elif k == 'up':  # an unfused upsample may write a slice of a concat buffer
                 ops.append(self._copy_op(node.inputs[0], node.out, node.out.coff, scale=2))
             elif k == 'concat':
@@ -690,18 +693,49 @@ class Engine:
         self.op_info.append(dict(kind='stem2', name='stem2_fused', flops=fs + fc, shape=shape, parts=2))
         return op
 
-    def _pool_op(self, node):
+    def _pool_cascades(self):
+        """Chains of 'same' stride-1 pools (the SPPCSPC k5 cascade, `pyramid`), each pool
+        reading the previous one's output, written to adjacent slices of one buffer: run as
+        one ycx_maxpool launch with levels = chain length (bf16 / fp8 plans, HIP_CASCADE
+        kernel). Returns {id(first pool): [pool nodes]}."""
+        if self.dt not in (L.DT_BF16, L.DT_FP8) or os.environ.get('YCX_NO_POOL_CASCADE'):
+            return {}
+        nodes, out = self.graph.nodes, {}
+        used = set()
+
+        def same_pool(nd):
+            p = nd.p
+            return nd.kind == 'pool' and p['s'] == 1 and p['k'] % 2 == 1 and p['p'] == p['k'] // 2
+
+        for i, a in enumerate(nodes):
+            if id(a) in used or not same_pool(a) or a.out.role in ('input', 'output'):
+                continue
+            chain = [a]
+            for b in nodes[i + 1:]:
+                prev = chain[-1]
+                if not (same_pool(b) and b.p['k'] == a.p['k'] and b.inputs[0] is prev.out and
+                        b.out.buf is a.out.buf and b.out.coff == prev.out.coff + prev.out.c and
+                        b.out.role not in ('input', 'output')):
+                    break
+                chain.append(b)
+            if len(chain) > 1:
+                out[id(a)] = chain
+                used.update(id(nd) for nd in chain)
+        return out
+
+    def _pool_op(self, node, levels=1):
         x, out, p = node.inputs[0], node.out, node.p
         d = L.PoolDesc()
         d.n, d.h, d.w, d.c, d.in_c_off, d.in_c_stride = x.n, x.h, x.w, x.c, x.coff, x.buf.c
         d.ho, d.wo, d.out_c_off, d.out_c_stride = out.h, out.w, out.coff, out.buf.c
-        d.k, d.stride, d.pad, d.dtype = p['k'], p['s'], p['p'], self.dt
+        d.k, d.stride, d.pad, d.dtype, d.levels = p['k'], p['s'], p['p'], self.dt, levels
         op = L.Op()
         op.kind = L.OP_POOL
         op.d.pool = d
         op.in_, op.out = x.buf.tensor.data_ptr(), out.buf.tensor.data_ptr()
-        self.op_info.append(dict(kind='pool', name=f"maxpool_k{p['k']}s{p['s']}", flops=0,
-                                 bytes=(x.n * (x.h * x.w + out.h * out.w) * x.c * self.dtype.itemsize)))
+        name = f"maxpool_k{p['k']}s{p['s']}" + (f"_cascade{levels}" if levels > 1 else "")
+        self.op_info.append(dict(kind='pool', name=name, flops=0,
+                                 bytes=(x.n * (x.h * x.w + levels * out.h * out.w) * x.c * self.dtype.itemsize)))
         return op
 
     def _copy_op(self, x, out, off, scale, nchw=False):
