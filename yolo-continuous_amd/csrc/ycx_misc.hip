@@ -61,6 +61,38 @@ __global__ void __launch_bounds__(256) maxpool_kernel(ycx_pool_desc d, const T* 
   }
 }
 
+// The same pool on a 2-D grid: blockIdx.y = output row (n * ho + oy), x over (ox, channel
+// chunk) -- 32-bit index math (the flat kernel's 64-bit div/mod chain was a VALU cost on the
+// HBM-bound k2s2 pools).
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_rows_kernel(ycx_pool_desc d, const T* __restrict__ x,
+                                                           T* __restrict__ y) {
+  typedef typename Vec<T>::type V;
+  constexpr int VN = Vec<T>::N;
+  const int cv = d.c / VN;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.wo * cv) return;
+  const int row = blockIdx.y, n = row / d.ho, oy = row - n * d.ho;
+  const int ox = i / cv, c = i - ox * cv;
+  float m[VN];
+#pragma unroll
+  for (int j = 0; j < VN; ++j) m[j] = -INFINITY;
+  const int y0 = oy * d.stride - d.pad, x0 = ox * d.stride - d.pad;
+  const int ya = max(y0, 0), yb = min(y0 + d.k, d.h), xa = max(x0, 0), xb = min(x0 + d.k, d.w);
+  for (int iy = ya; iy < yb; ++iy) {
+    const T* rowp = x + ((size_t)(n * d.h + iy) * d.w) * d.in_c_stride + d.in_c_off + c * VN;
+    for (int ix = xa; ix < xb; ++ix) {
+      const V v = *reinterpret_cast<const V*>(rowp + (size_t)ix * d.in_c_stride);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) m[j] = fmaxf(m[j], (float)v[j]);
+    }
+  }
+  V o;
+#pragma unroll
+  for (int j = 0; j < VN; ++j) o[j] = (T)m[j];
+  *reinterpret_cast<V*>(y + ((size_t)row * d.wo + ox) * d.out_c_stride + d.out_c_off + c * VN) = o;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) copy_kernel(ycx_copy_desc d, const T* __restrict__ x,
                                                    T* __restrict__ y) {
@@ -300,6 +332,16 @@ extern "C" ycx_status ycx_maxpool(const ycx_pool_desc* d, const void* x, void* y
     return ycx_launch_status();
   }
   long long total = (long long)d->n * d->ho * d->wo * (d->c / vn);
+  const long long rows = (long long)d->n * d->ho, rowlen = (long long)d->wo * (d->c / vn);
+  if (d->dtype != YCX_DT_FP8 && rows <= 65535 && total < (1LL << 31) &&
+      (long long)d->n * d->h * d->w * d->in_c_stride < (1LL << 31)) {
+    const dim3 g((unsigned)((rowlen + 255) / 256), (unsigned)rows);
+    if (d->dtype == YCX_DT_BF16)
+      hipLaunchKernelGGL(maxpool_rows_kernel<__bf16>, g, dim3(256), 0, st, *d, (const __bf16*)x, (__bf16*)y);
+    else
+      hipLaunchKernelGGL(maxpool_rows_kernel<float>, g, dim3(256), 0, st, *d, (const float*)x, (float*)y);
+    return ycx_launch_status();
+  }
   if (d->dtype == YCX_DT_FP8)
     hipLaunchKernelGGL(maxpool_f8_kernel, dim3(grid_for(total)), dim3(256), 0, st, *d, (const uint8_t*)x,
                        (uint8_t*)y);
