@@ -23,7 +23,7 @@ from ycx.utils.synth import synthetic_images
 
 pytestmark = pytest.mark.gpu
 A = np.asarray(ANCHORS).reshape(-1, 2)
-C2_BAR, C5_BAR = 5e-2, 0.10   # heads: max |gpu - oracle| / max |oracle| (bf16, fp8 e4m3)
+C2_BAR, C5_BAR = 1e-2, 0.10   # heads: max |gpu - oracle| / max |oracle| (bf16, fp8 e4m3); measured r02: 0.0045, 0.088
 KEEP_FLIPS_PIN = {'c2': 6, 'c5': 4, 'c4': 12}   # measured on MI355X: 3/0, 0/0, 6
 
 

@@ -10,7 +10,8 @@ Oracle levels:
     one code away; fp32 head outputs within 1e-4 of max |ref|;
   * the whole network vs the fp32 oracle (the reference's own forward restated):
     e4m3 keeps 3 mantissa bits per activation and weight, so per-head error is
-    bounded at FP8_TOL of max |ref| (measured ~half of it on the seeded weights).
+    bounded at FP8_TOL of max |ref| (measured on MI355X, r02: 0.054-0.095 over the G1 nets,
+    0.062-0.086 on yolov7 640 bs 2).
 """
 import ctypes
 
@@ -28,7 +29,7 @@ from ycx.utils.synth import synthetic_images
 pytestmark = pytest.mark.gpu
 L = pytest.importorskip("ycx._lib")
 E4M3 = torch.float8_e4m3fn
-FP8_TOL = 0.15
+FP8_TOL = 0.12   # 1.26x the largest measured error (G1 csp_blocks 0.095)
 
 
 def _q(x, s=1.0):
@@ -222,6 +223,7 @@ def test_g1_ops_fp8(device, manifest, g1, name):
     for j, o in enumerate(outs):
         gold = torch.from_numpy(g1[f'{name}/{j}'])
         assert o.shape == gold.shape
+        print(f"\nfp8 G1 {name} out {j} rel err {rel_err(o.cpu(), gold):.4f}")
         assert rel_err(o.cpu(), gold) < FP8_TOL, (name, j, rel_err(o.cpu(), gold))
 
 
