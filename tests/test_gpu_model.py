@@ -2,8 +2,8 @@
 
 Tolerances (max |gpu - ref| / max |ref| per output tensor):
   f32 parity mode : 1e-3  (north_star: 1e-3 relative on box/confidence tensors)
-  bf16            : 5e-2  (bf16 activations/weights drift ~0.5 % median, ~1 % of
-                           max-abs end to end through 100+ layers)
+  bf16            : 2.5e-2 (bf16 activations/weights drift ~0.5 % median, up to 1.25 % of
+                           max-abs end to end through 100+ layers: measured r02 max 0.0125)
 """
 import numpy as np
 import pytest
@@ -16,7 +16,7 @@ from ycx.utils.synth import synthetic_images
 
 pytestmark = pytest.mark.gpu
 
-F32_TOL, BF16_TOL = 1e-3, 5e-2
+F32_TOL, BF16_TOL = 1e-3, 2.5e-2   # bf16 measured r02: <= 0.0125 (G2 tiny_640), yolov7 heads ~0.005
 G1_NAMES = ['conv_k3s1_cin32', 'conv_k3s2_cin32', 'conv_k1_cin64', 'conv_leaky', 'stem_s2_leaky', 'pools',
             'upsample_concat', 'upsample_shared', 'sppcspc', 'repconv', 'csp_blocks', 'detect', 'idetect',
             'upsample_offset', 'iauxdetect']
@@ -52,6 +52,7 @@ def test_g1_ops(device, manifest, g1, name, precision, tol):
         gold = torch.from_numpy(g1[f'{name}/{j}'])
         o = o.cpu()
         assert o.shape == gold.shape
+        print(f"\n{precision} G1 {name} out {j} rel err {rel_err(o, gold):.5f}")
         assert rel_err(o, gold) < tol, (name, j, rel_err(o, gold))
 
 
@@ -66,10 +67,11 @@ def test_g2_nets(device, manifest, g2, name, precision, tol):
     for j, o in enumerate(outs):
         gold = torch.from_numpy(g2[f'{name}/{j}'])
         assert tuple(o.shape) == tuple(gold.shape)
+        print(f"\n{precision} G2 {name} out {j} rel err {rel_err(o.cpu(), gold):.5f}")
         assert rel_err(o.cpu(), gold) < tol, (name, j, rel_err(o.cpu(), gold))
 
 
-DECODED_TOL = {'f32': 1e-3, 'bf16': 2e-2}   # decoded box / confidence tensors, max |gpu - ref| / max |ref|
+DECODED_TOL = {'f32': 1e-3, 'bf16': 5e-3}   # decoded box / confidence tensors, max |gpu - ref| / max |ref|; r02: 6e-7, 1.1e-3
 
 
 @pytest.mark.parametrize('precision,tol', [('f32', F32_TOL), ('bf16', BF16_TOL)])
