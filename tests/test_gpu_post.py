@@ -273,15 +273,16 @@ def _sorted_cands(det, b):
     return rows, det.cand[b].cpu()[rows.long()]   # ycx_cand is indexed by row, cand_rows lists the rows
 
 
+@pytest.mark.parametrize('precision', ['bf16', 'fp8'])
 @pytest.mark.parametrize('cfg,nc,shape', [('yolov7-tiny', 1, (3, 3, 224, 224)), ('yolov7-tiny', 80, (2, 3, 320, 256)),
                                           ('yolov7', 80, (2, 3, 256, 256))])
-def test_head_decode_fused_in_conv(device, cfg, nc, shape):
+def test_head_decode_fused_in_conv(device, cfg, nc, shape, precision):
     """ycx_conv2d_head (decode + filter in the Detect-head conv epilogue) vs the
     unfused chain (head conv -> fp32 NCHW heads -> ycx_decode_filter) on the
     same model and images: raw heads, candidate rows and values, keep rows and
     dets are all bit-identical, with and without the raw-head store. 224 and
     320x256 put 64-pixel head tiles across image boundaries (7x7, 10x8 grids)."""
-    m, _ = make_model(cfg, nc, 0, 'bf16')
+    m, _ = make_model(cfg, nc, 0, precision)
     m.to(device)
     x = synthetic_images(*shape, seed=31).to(device)
     conf = 0.3 if nc == 1 else 0.05   # random-init nc=80 scores are ~0.5*0.5; keep the filter busy

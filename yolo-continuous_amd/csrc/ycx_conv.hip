@@ -1055,8 +1055,8 @@ __device__ __forceinline__ void epilogue_f8(const ConvArgs& a, const f32x4 (&acc
   }
 }
 
-template <int BM, int BN, int WM, int WN, int TPS>
-__global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a) {
+template <int BM, int BN, int WM, int WN, int TPS, bool HEAD = false>
+__global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a, HeadArgs hd) {
   constexpr int NW = WM * WN, NST = 2;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(TPS == 0 || TPS == 1 || TPS == 2 || TPS == 4, "taps per K step (0: any cin % 16 == 0)");
@@ -1185,8 +1185,37 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a) {
     __builtin_amdgcn_sched_barrier(0);
   }
   static_assert(FM % 2 == 0, "fragment pairs");
-  if (perm) epilogue_f8x8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
-  else epilogue_f8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+  if constexpr (HEAD) {
+    // Detect head (tile 39): the fp32 logits act(acc * dq + bias) of all BM channels of BN
+    // pixels to LDS (the unfused epilogue_f8's expression, so the candidates are the same),
+    // then the decode + filter of conv_bf16_glds's head tile
+    constexpr int HEAD_LDT = BN + 1;
+    static_assert(BM * HEAD_LDT * 4 + 34 * 4 <= NST * STAGE, "head tile (+ append counts) fits the stages");
+    const float* dq = a.bias + a.Cout_pad;
+    f32x4 bb[FM], qq[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int co = co0 + wm * TM + i * 16 + (lane >> 4) * 4;
+      bb[i] = *reinterpret_cast<const f32x4*>(a.bias + co);
+      qq[i] = *reinterpret_cast<const f32x4*>(dq + co);
+    }
+    __syncthreads();  // every wave is past its last fragment read: the stages become the logit tile
+    float* T = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          T[co * HEAD_LDT + wn * TN + j * 16 + (lane & 15)] = fmaf(acc[i][j][r], qq[i][r], bb[i][r]);
+      }
+    __syncthreads();
+    head_decode_tile<BN>(a, hd, T, HEAD_LDT, px0);
+  } else {
+    if (perm) epilogue_f8x8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+    else epilogue_f8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+  }
 }
 
 #ifdef YCX_EXPERIMENTAL_TILES  // retired: measured 0.5-0.9x of the picked tiles
@@ -2687,6 +2716,7 @@ const TileInfo kTiles[] = {
     {32, 64, 128, "f8_wres1x1"},
     {64, 256, 64, "f8_halo3x3_ws_co64"},
     {256, 64, 64, "head_co256_px64_decode"},
+    {256, 64, 128, "f8_head_co256_px64_decode"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -2742,8 +2772,17 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
-// tile 38: Detect head conv (all <= 256 channels of BN = 64 pixels per workgroup) + decode + filter
-ycx_status launch_head(ConvArgs a, const HeadArgs& hd, hipStream_t st) {
+// tile 38 (bf16) / 39 (e4m3): Detect head conv (all <= 256 channels of BN = 64 pixels per
+// workgroup) + decode + filter
+ycx_status launch_head(ConvArgs a, const HeadArgs& hd, hipStream_t st, bool f8) {
+  if (f8) {  // one 128-channel K step per tap (cin % 128 == 0), weight rows of whole K steps
+    if (a.Cin % 128 || a.Cout_pad != 256 || a.Cout > 256 || a.Ktot != a.Cin) return YCX_ERR_UNSUPPORTED;
+    a.nsteps = a.Cin / 128;
+    a.n_ct = 1;
+    a.nwg = (a.M + 63) / 64;
+    hipLaunchKernelGGL((conv_f8_glds<256, 64, 4, 2, 1, true>), dim3(a.nwg), dim3(512), 0, st, a, hd);
+    return ycx_launch_status();
+  }
   if (a.Cin % 64 || a.Cout_pad != 256 || a.Cout > 256) return YCX_ERR_UNSUPPORTED;
   a.nsteps = a.KH * a.KW * (a.Cin / 64);
   a.n_ct = 1;
@@ -2765,10 +2804,10 @@ ycx_status launch_f8(ConvArgs a, hipStream_t st) {
   a.n_ct = a.Cout_pad / BM;
   a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
   const dim3 g(a.nwg), b(WM * WN * 64);
-  if (tps == 4) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 4>), g, b, 0, st, a);
-  else if (tps == 2) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 2>), g, b, 0, st, a);
-  else if (tps == 1) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 1>), g, b, 0, st, a);
-  else hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 0>), g, b, 0, st, a);
+  if (tps == 4) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 4>), g, b, 0, st, a, HeadArgs{});
+  else if (tps == 2) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 2>), g, b, 0, st, a, HeadArgs{});
+  else if (tps == 1) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 1>), g, b, 0, st, a, HeadArgs{});
+  else hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 0>), g, b, 0, st, a, HeadArgs{});
   return ycx_launch_status();
 }
 
@@ -2944,7 +2983,7 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
     // 20^2 x bs 32: 3x3 256->256 0.037 -> 0.027 ms, 512->256 0.068 -> 0.046 ms against co128 x px64)
     return 18;
   }
-  if ((M + 255) / 256 >= 2048) return 15;
+  if ((M + 255) / 256 >= 512) return 15;  // tests/probes/conv_bench.py: 80^2 x bs 32 128->64 3x3 48.7 vs 52.3 us (t18)
   if ((d->cout_pad / 64) * ((M + 127) / 128) >= 256) return 18;
   return 3;
 }
@@ -3050,16 +3089,18 @@ extern "C" ycx_status ycx_conv2d_head(const ycx_conv_desc* d, const ycx_head_des
   YCX_CHECK_ARG(d->in_c_off >= 0 && d->in_c_off + d->cin <= d->in_c_stride && d->cout_pad >= d->cout);
   YCX_CHECK_ARG(h->na > 0 && h->na <= 8 && h->nc > 0 && h->no == h->nc + 5 && h->na * h->no == d->cout);
   YCX_CHECK_ARG(h->row_off >= 0 && h->row_off + h->na * d->ho * d->wo <= h->rows_total);
-  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0);
+  const bool f8 = d->dtype == YCX_DT_FP8;
+  YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_BF16 || f8) && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0);
   YCX_CHECK_SUPPORTED(d->act == YCX_ACT_NONE && d->out_layout == YCX_OUT_NCHW_F32 && d->cout_pad == 256);
-  YCX_CHECK_SUPPORTED(d->in_c_off % 8 == 0 && d->in_c_stride % 8 == 0);
+  YCX_CHECK_SUPPORTED(f8 ? (d->in_c_off % 16 == 0 && d->in_c_stride % 16 == 0)
+                         : (d->in_c_off % 8 == 0 && d->in_c_stride % 8 == 0));
   YCX_CHECK_SUPPORTED((long long)d->n * d->h * d->w * d->in_c_stride * 2 < (1LL << 31));
   YCX_CHECK_SUPPORTED((long long)d->n * h->rows_total < (1LL << 31));
   ConvArgs a = make_args(d, x, w, bias, heads, nullptr);
   a.out_coff = 0;
   a.out_cs = d->cout;
   HeadArgs hd{*h, cand, cand_rows, cand_counts, heads};
-  return launch_head(a, hd, reinterpret_cast<hipStream_t>(stream));
+  return launch_head(a, hd, reinterpret_cast<hipStream_t>(stream), f8);
 }
 
 extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, const float* w, const float* bias,

@@ -272,7 +272,7 @@ class Detector:
     """Fused device pipeline for a fixed batch shape: Model forward (static plan,
     optionally one HIP graph) -> candidates -> ycx_sort_nms (DevicePost).
 
-    bf16 Detect models decode in the head convs (``fuse_heads``, default): each
+    bf16 and fp8 Detect models decode in the head convs (``fuse_heads``, default): each
     head level's ycx_conv2d_head appends that level's candidates straight from
     the fp32 logits held on chip (detect.py:29-121), so the forward ends with
     the candidate list and the post is the NMS alone. ``keep_heads`` also

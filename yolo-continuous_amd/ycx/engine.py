@@ -770,10 +770,11 @@ class Engine:
 
     # ---- fused Detect heads (decode + candidate filter in the head conv) ----
     def head_ops(self):
-        """Op index of each output's producing conv, when every output is a bf16
-        Detect-head 1x1 conv the fused kernel covers (ycx_conv2d_head), else None."""
-        if self.dt != L.DT_BF16:
+        """Op index of each output's producing conv, when every output is a bf16 or
+        e4m3 Detect-head 1x1 conv the fused kernels cover (ycx_conv2d_head), else None."""
+        if self.dt not in (L.DT_BF16, L.DT_FP8):
             return None
+        f8 = self.dt == L.DT_FP8
         idx = []
         for v in self.out_vals:
             slots = self.output_slots.get(id(v), [])
@@ -783,7 +784,8 @@ class Engine:
             d = op.d.conv
             if not (op.kind == L.OP_CONV and d.kh == 1 and d.kw == 1 and d.stride == 1 and d.pad == 0 and
                     d.act == L.ACT_NONE and d.out_layout == L.OUT_NCHW_F32 and d.cout <= 256 and
-                    d.cin % 64 == 0 and d.in_c_off % 8 == 0 and d.in_c_stride % 8 == 0):
+                    d.cin % (128 if f8 else 64) == 0 and d.in_c_off % (16 if f8 else 8) == 0 and
+                    d.in_c_stride % (16 if f8 else 8) == 0):
                 return None
             idx.append(slots[0][0])
         return idx
@@ -807,15 +809,22 @@ class Engine:
                 wi = next(j for j, t in enumerate(self.params) if t.data_ptr() == op.weight)
                 w, b = self.params[wi], self.params[wi + 1]
                 w2 = torch.zeros((256,) + tuple(w.shape[1:]), dtype=w.dtype, device=w.device)
-                b2 = torch.zeros((256,), dtype=b.dtype, device=b.device)
-                w2[:conv.cout], b2[:conv.cout] = w[:conv.cout], b[:conv.cout]
+                if self.dt == L.DT_FP8:  # bias then dq, each [cout_pad]
+                    b2 = torch.zeros((512,), dtype=b.dtype, device=b.device)
+                    b2[:conv.cout] = b[:conv.cout]
+                    b2[256:256 + conv.cout] = b[conv.cout_pad:conv.cout_pad + conv.cout]
+                else:
+                    b2 = torch.zeros((256,), dtype=b.dtype, device=b.device)
+                    b2[:conv.cout] = b[:conv.cout]
+                w2[:conv.cout] = w[:conv.cout]
                 self.head_params += [w2, b2]   # self.params keeps the plan's shapes (prepack)
                 op.weight, op.bias, conv.cout_pad = w2.data_ptr(), b2.data_ptr(), 256
             op.kind = L.OP_HEAD
             op.d.head.conv = conv
             op.d.head.head = hd
             op.cand, op.cand_rows, op.cand_counts = cand.data_ptr(), cand_rows.data_ptr(), counts.data_ptr()
-            self.op_info[i] = dict(self.op_info[i], name=L.lib.ycx_conv_tile_name(38).decode(), kind='head')
+            tile = 39 if self.dt == L.DT_FP8 else 38
+            self.op_info[i] = dict(self.op_info[i], name=L.lib.ycx_conv_tile_name(tile).decode(), kind='head')
             if not keep_heads:
                 self.head_unstored.add(i)
         if self.fixed_outputs is not None:
