@@ -2852,7 +2852,13 @@ bool wres_ok(const ConvArgs& a) {
 // 160^2 256->128 0.17 -> 0.13 ms against tile 16
 ycx_status launch_wres(ConvArgs a, hipStream_t st) {
   if (!wres_ok(a)) return YCX_ERR_UNSUPPORTED;
-  if (a.Cout_pad % 256 == 0) return launch_wres_k<8, 1, 64, 5, 2>(a, st);  // 16 KB stages
+#ifndef YCX_WRES_NS  // ring depth of the 256-channel-group variant (development A/B knob)
+#define YCX_WRES_NS 5
+#endif
+#ifndef YCX_WRES_TPW
+#define YCX_WRES_TPW 64
+#endif
+  if (a.Cout_pad % 256 == 0) return launch_wres_k<8, 1, YCX_WRES_TPW, YCX_WRES_NS, 2>(a, st);  // 16 KB stages
   if (a.Cout_pad == 128) return launch_wres_k<4, 2, 64, 6, 1>(a, st);
   return launch_wres_k<2, 4, 32, 6, 1>(a, st);
 }
