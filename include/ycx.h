@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define YCX_ABI_VERSION 5
+#define YCX_ABI_VERSION 6
 
 typedef int32_t ycx_status;
 enum {
@@ -87,6 +87,9 @@ typedef struct ycx_conv_desc {
   int32_t tile;             /* 0 = auto, else a tile id (see ycx_conv_tile_name)    */
   float out_scale;          /* YCX_DT_FP8 only: output quantisation scale          */
   float res_scale;          /* YCX_DT_FP8 only: residual dequantisation (1 / s_res) */
+  int32_t in_pool;          /* 1: x is the (2h, 2w) map that MP's k2 s2 max-pool reduces to the
+                             * (h, w) input (nets/common.py:25-31), pooled in the conv's operand
+                             * staging (bf16 1x1/s1/p0, cin % 64 == 0); 0: x is the input */
 } ycx_conv_desc;
 
 /* Max-pool, NHWC, pad value -inf (torch.nn.MaxPool2d semantics, floor mode).

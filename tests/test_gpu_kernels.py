@@ -224,6 +224,76 @@ def test_maxpool_cascade(device, hw, c, k, fp8):
     assert not got[..., :32].any()  # channels before out_c_off untouched
 
 
+@pytest.mark.parametrize('tile', [0, 16, 18])
+@pytest.mark.parametrize('n,hw,cin,cout', [(2, (13, 11), 64, 128), (3, (20, 20), 256, 128), (1, (8, 40), 128, 256),
+                                           (2, (10, 10), 512, 256), (1, (5, 7), 64, 64)])
+def test_conv_pool_fused(device, tile, n, hw, cin, cout):
+    """MP fused into the 1x1 conv (ycx_conv_desc.in_pool: the k2 s2 max-pool of the (2h, 2w)
+    map formed in the operand staging) vs ycx_maxpool then the same tile on the pooled map:
+    bit for bit (the max is exact, the MFMA sees identical operands in the same order), and
+    vs the float64 reference of pool + conv. Ragged pixel tails, channel-sliced input."""
+    g = torch.Generator().manual_seed(11)
+    (h, w), ex = hw, 16
+    x = (torch.randn(n, 2 * h, 2 * w, cin + ex, generator=g) * 2).to(torch.bfloat16)
+    wt = (torch.randn(cout, cin, generator=g) / cin ** 0.5).to(torch.bfloat16)
+    b = torch.randn(cout, generator=g) * 0.1
+    cpad = 64 if cout <= 64 else -(-cout // 128) * 128
+    if tile == 16 and cpad % 128:
+        pytest.skip("tile 16 is 128 output channels wide")
+    wp = torch.zeros(cpad, cin, dtype=torch.bfloat16)
+    wp[:cout] = wt
+    bp = torch.zeros(cpad)
+    bp[:cout] = b
+    xd, wd, bd = x.to(device), wp.to(device), bp.to(device)
+    pooled = torch.zeros(n, h, w, cin, dtype=torch.bfloat16, device=device)
+    pd = L.PoolDesc()
+    pd.n, pd.h, pd.w, pd.c, pd.in_c_off, pd.in_c_stride = n, 2 * h, 2 * w, cin, ex, cin + ex
+    pd.ho, pd.wo, pd.out_c_off, pd.out_c_stride, pd.k, pd.stride, pd.pad, pd.dtype = h, w, 0, cin, 2, 2, 0, L.DT_BF16
+    pd.levels = 1
+    L.check(L.lib.ycx_maxpool(ctypes.byref(pd), xd.data_ptr(), pooled.data_ptr(), L.stream_handle(device)))
+
+    def conv(src, in_off, in_stride, in_pool):
+        y = torch.zeros(n, h, w, cout + 8, dtype=torch.bfloat16, device=device)
+        d = L.ConvDesc()
+        d.n, d.h, d.w, d.cin, d.in_c_off, d.in_c_stride = n, h, w, cin, in_off, in_stride
+        d.ho, d.wo, d.cout, d.cout_pad, d.out_c_off, d.out_c_stride = h, w, cout, cpad, 8, cout + 8
+        d.kh = d.kw = d.stride = 1
+        d.pad, d.act, d.leaky_slope, d.dtype, d.out_layout = 0, L.ACT_SILU, 0.1, L.DT_BF16, L.OUT_NHWC
+        d.in_pool = in_pool
+        d.tile = tile if tile else int(L.lib.ycx_conv_pick_tile(ctypes.byref(d)))
+        L.check(L.lib.ycx_conv2d(ctypes.byref(d), src.data_ptr(), wd.data_ptr(), bd.data_ptr(), y.data_ptr(), None,
+                                 L.stream_handle(device)))
+        return y, d.tile
+
+    fused, tile = conv(xd, ex, cin + ex, 1)  # auto: the unfused call runs the tile the fused one picked
+    assert tile in (16, 18)
+    unfused = conv(pooled, 0, cin, 0)[0]
+    torch.cuda.synchronize()
+    assert torch.equal(fused.cpu(), unfused.cpu())
+    assert not fused.cpu()[..., :8].any()
+    ref = F.silu(F.conv2d(F.max_pool2d(x[..., ex:].permute(0, 3, 1, 2).double(), 2, 2), wt.double()[..., None, None],
+                          b.double()))
+    torch.testing.assert_close(fused.cpu()[..., 8:].permute(0, 3, 1, 2).double(), ref, rtol=1e-2, atol=1e-2)
+
+
+def test_conv_pool_fused_rejects(device):
+    """in_pool is a bf16 1x1 / s1 / p0 feature of tiles 16 / 18 / 25."""
+    d = L.ConvDesc()
+    d.n, d.h, d.w, d.cin, d.in_c_stride, d.ho, d.wo, d.cout, d.cout_pad = 1, 8, 8, 64, 64, 8, 8, 128, 128
+    d.out_c_stride, d.kh, d.kw, d.stride, d.pad, d.dtype, d.in_pool = 128, 1, 1, 1, 0, L.DT_BF16, 1
+    t = torch.zeros(1 << 16, device=device)
+    call = lambda: L.lib.ycx_conv2d(ctypes.byref(d), t.data_ptr(), t.data_ptr(), t.data_ptr(), t.data_ptr(), None,
+                                    L.stream_handle(device))
+    d.tile = 22
+    assert call() == L.YCX_ERR_UNSUPPORTED
+    d.tile, d.dtype = 0, L.DT_F32
+    assert call() == L.YCX_ERR_UNSUPPORTED
+    d.dtype, d.kh, d.kw, d.pad = L.DT_BF16, 3, 3, 1
+    assert call() == L.YCX_ERR_UNSUPPORTED
+    d.kh, d.kw, d.pad, d.in_pool = 1, 1, 0, 2
+    assert call() == L.YCX_ERR_BAD_ARG
+
+
 @pytest.mark.parametrize('dtype', [L.DT_BF16, L.DT_F32])
 @pytest.mark.parametrize('scale,nchw', [(1, False), (2, False), (1, True)])
 def test_copy_upsample(device, dtype, scale, nchw):

@@ -113,6 +113,28 @@ def test_engine_plan_properties(device):
     assert sum(i.get('parts', 1) for i in eng.op_info if i['kind'] in ('conv', 'stem', 'stem2')) == 92
     assert sum(1 for i in eng.op_info if i['kind'] == 'conv' and i['parts'] == 2) == 8
     assert abs(s['gflop_per_image'] - 104.511078400) < 1e-6
+    # the five MP k2 s2 pools run inside their 1x1 consumers; the SPPCSPC cascade is the one pool op
+    assert sum(1 for i in eng.op_info if i['name'].endswith('+maxpool_k2s2')) == 5
+    assert [i['name'] for i in eng.op_info if i['kind'] == 'pool'] == ['maxpool_k5s1_cascade3']
+
+
+def test_pool_fusion_bit_identical(device):
+    """yolov7 bf16 plan with the MP pools fused into their 1x1 convs == the plan that runs
+    them as ycx_maxpool ops, bit for bit."""
+    from ycx.engine import Engine
+    m, _ = make_model('yolov7', 80, 0, 'bf16')
+    m.to(device)
+    x = synthetic_images(2, 3, 320, 320, seed=4).to(device)
+    outs = []
+    for fuse in (True, False):
+        eng = Engine(m, tuple(x.shape), torch.device(device), 'bf16', fuse_pool=fuse)
+        try:
+            assert sum(1 for i in eng.op_info if i['name'].endswith('+maxpool_k2s2')) == (5 if fuse else 0)
+            outs.append([o.clone() for o in eng.run(x)])
+        finally:
+            eng.close()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 def test_graph_replay_matches_eager(device):

@@ -43,6 +43,7 @@ struct ConvArgs {
   int res_coff, res_cs;
   int M, HoWo, Ktot, nsteps, n_ct, nwg;
   float out_scale, res_scale;  // YCX_DT_FP8 only
+  int pool;                    // x is the (2H, 2W) map of a fused k2 s2 max-pool (ycx_conv_desc.in_pool)
 };
 
 template <int BK>
@@ -621,7 +622,12 @@ __device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const fl
 // tap fetches zeros on the activation side (its weight chunk is finite).
 // NST = 2 halves the LDS so two workgroups share a CU: one block's prologue
 // and epilogue then overlap the other's MFMA loop (short-K layers).
-template <int BM, int BN, int WM, int WN, bool TT, int NST, int NSB = NST, bool HEAD = false>
+// POOL (1x1 / s1 / p0 only): the activation operand is MP's k2 s2 max-pool of the
+// (2H, 2W) map x (nets/common.py:25-31), formed while staging: step t issues the
+// weight DMA of t + 1 and four 16-byte global loads per pixel row (the 2x2 window),
+// and after step t's MFMAs takes their max and writes it to the LDS slot where the
+// activation DMA would have put it. The pooled map never reaches HBM.
+template <int BM, int BN, int WM, int WN, bool TT, int NST, int NSB = NST, bool HEAD = false, bool POOL = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadArgs hd) {
   constexpr int NW = WM * WN;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
@@ -642,6 +648,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   constexpr int HEAD_LDT = BN + 1;  // HEAD: fp32 logits [BM][BN + 1] (odd stride: conflict-free writes)
   static_assert(!HEAD || BM * HEAD_LDT * 4 + 34 * 4 <= LDS_BYTES, "head tile (+ append counts) fits the stages");
   static_assert(!HEAD || NW <= 16, "head append counts: 16 waves");
+  static_assert(!POOL || (NST == 2 && !SPLIT && !TT && !HEAD), "pooled operand: two-stage [A | B] ring");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
   const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
@@ -685,7 +692,10 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     b_iy0[i] = ok ? oy * a.S - a.P : -(1 << 20);  // tail rows fail the bounds test
     b_ix0[i] = ox * a.S - a.P;
     const int lch = pch ^ swz<BK>(row);  // logical chunk this lane fetches
-    b_base[i] = (((n * a.H + b_iy0[i]) * a.W + b_ix0[i]) * a.in_cs + a.in_coff + ((TT ? lch & 3 : lch) << 3)) * 2;
+    if constexpr (POOL)  // element offset of the window's top-left pixel; -1: tail row (zeros)
+      b_base[i] = ok ? ((n * 2 * a.H + 2 * oy) * 2 * a.W + 2 * ox) * a.in_cs + a.in_coff + (lch << 3) : -1;
+    else
+      b_base[i] = (((n * a.H + b_iy0[i]) * a.W + b_ix0[i]) * a.in_cs + a.in_coff + ((TT ? lch & 3 : lch) << 3)) * 2;
   }
   // swz<64>(row) = (4 wid + lrow / 2) & 7 for every i: one tap select per lane.
   const bool sel1 = TT && ((pch ^ swz<BK>(8 * wid + lrow)) >> 2);
@@ -733,6 +743,33 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     issueA(s, buf);
     issueB(buf);
   };
+  // POOL: the window's four rows of the next K step in flight in registers (no VALU on
+  // them before the MFMAs, which would wait for the loads), pooled into LDS after them
+  bf16x8 pw[POOL ? B_PW : 1][4];
+  auto loadB = [&]() {
+    const int cs = a.in_cs, rs = 2 * a.W * a.in_cs;
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      const __bf16* src = X + (b_base[i] < 0 ? 0 : b_base[i] + i_cb);
+      pw[i][0] = *reinterpret_cast<const bf16x8*>(src);
+      pw[i][1] = *reinterpret_cast<const bf16x8*>(src + cs);
+      pw[i][2] = *reinterpret_cast<const bf16x8*>(src + rs);
+      pw[i][3] = *reinterpret_cast<const bf16x8*>(src + rs + cs);
+    }
+    i_cb += BK;
+  };
+  auto writeB = [&](int buf) {
+    char* base = b_slot(buf);
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = (__bf16)fmaxf(fmaxf((float)pw[i][0][j], (float)pw[i][1][j]), fmaxf((float)pw[i][2][j], (float)pw[i][3][j]));
+      if (b_base[i] < 0) v = bf16x8{};
+      *reinterpret_cast<bf16x8*>(base + (wid + NW * i) * 1024 + lane * 16) = v;
+    }
+  };
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -745,11 +782,15 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   if constexpr (HEAD) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) bpre[i] = *reinterpret_cast<const f32x4*>(a.bias + co0 + wm * TM + i * 16 + (lane >> 4) * 4);
-  } else if constexpr (FM % 2 == 0) {
+  } else if constexpr (FM % 2 == 0 && !POOL) {  // POOL: no registers to spare, loaded after the loop
     if (perm) bias8_prefetch<FM>(a, co0 + wm * TM, lane, bpre);
   }
   const int nt = a.nsteps;
-  if constexpr (SPLIT) {
+  if constexpr (POOL) {
+    issueA(0, 0);
+    loadB();
+    writeB(0);
+  } else if constexpr (SPLIT) {
     // prologue A0, B0, B1; step t issues A(t+1) then B(t+2), so at the top of step t the
     // wave's youngest outstanding DMA is B(t+1) (issued after A(t)): vmcnt(B_PW)
     issueA(0, 0);
@@ -779,6 +820,11 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     if constexpr (SPLIT) {
       if (t + 1 < nt) issueA(t + 1, (t + 1) % NST);
       if (t + 2 < nt) issueB((t + 2) % NSB);
+    } else if constexpr (POOL) {
+      if (t + 1 < nt) {
+        issueA(t + 1, (t + 1) % NST);
+        loadB();
+      }
     } else {
       // DMA issued first thing after the barrier: issuing it after the fragment reads or
       // between the MFMA halves measured 4-19 % slower (latency, not issue cost, binds)
@@ -821,6 +867,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     __builtin_amdgcn_s_setprio(0);
 #endif
     __builtin_amdgcn_sched_barrier(0);
+    // slot (t + 1) % 2 held step t - 1, which every wave finished before this step's barrier
+    if constexpr (POOL)
+      if (t + 1 < nt) writeB((t + 1) % NST);
     STAMP(5);
 #ifdef YCX_GLDS_STAMP
     stamp_sync();
@@ -855,6 +904,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   }
   if constexpr (FM % 2 == 0 && !HEAD) {
     if (perm) {
+      if constexpr (POOL) bias8_prefetch<FM>(a, co0 + wm * TM, lane, bpre);
       epilogue_regs8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane, bpre);
       done = true;
     }
@@ -2668,6 +2718,7 @@ ConvArgs make_args(const ycx_conv_desc* d, const void* x, const void* w, const f
   if (d->dtype == YCX_DT_FP8) a.Ktot = (a.Ktot + 127) / 128 * 128;  // padded weight row (bytes)
   a.nsteps = 0; a.n_ct = 0; a.nwg = 0;
   a.out_scale = d->out_scale; a.res_scale = d->res_scale;
+  a.pool = d->in_pool;
   return a;
 }
 
@@ -2767,6 +2818,15 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   a.nsteps = TT ? (a.KH * a.KW + 1) / 2 : a.KH * a.KW * (a.Cin / 64);
   a.n_ct = a.Cout_pad / BM;
   a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
+  if constexpr (!TT && NST == 2 && NSB == 2 && BN == 128) {  // tiles 16, 18, 25
+    if (a.pool) {
+      if (a.KH != 1 || a.KW != 1 || a.S != 1 || a.P != 0) return YCX_ERR_UNSUPPORTED;
+      hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, false, 2, 2, false, true>), dim3(a.nwg), dim3(WM * WN * 64),
+                         0, st, a, HeadArgs{});
+      return ycx_launch_status();
+    }
+  }
+  if (a.pool) return YCX_ERR_UNSUPPORTED;
   hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST, NSB>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a,
                      HeadArgs{});
   return ycx_launch_status();
@@ -2931,6 +2991,8 @@ extern "C" const char* ycx_conv_tile_name(int32_t tile) {
 static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wres: no residual (tiles 22, 23)
   if (d->dtype == YCX_DT_F32) return 8;
   const long long M = (long long)d->n * d->ho * d->wo;
+  if (d->in_pool)  // the pooled-operand variants of the two-stage LDS-DMA tiles
+    return d->cout_pad % 128 == 0 && (d->cout_pad / 128) * ((M + 127) / 128) >= 256 ? 16 : 18;
   if (d->dtype == YCX_DT_FP8) {
     // pointwise layers with cin in {128, 256, 512} and >= 8 pixel tiles per persistent block:
     // weights resident in registers (tile 36)
@@ -3021,11 +3083,17 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
   // The 32-bit index math inside the kernels.
   YCX_CHECK_SUPPORTED((long long)d->n * d->ho * d->wo < (1LL << 31));
   YCX_CHECK_SUPPORTED((long long)d->cout_pad * d->kh * d->kw * d->cin < (1LL << 31));
+  if (d->in_pool) {  // fused MP: bf16 pointwise over a (2h, 2w) map
+    YCX_CHECK_ARG(d->in_pool == 1);
+    YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0);
+    YCX_CHECK_SUPPORTED((long long)d->n * 4 * d->h * d->w * d->in_c_stride * 2 < (1LL << 31));
+  }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ConvArgs a = make_args(d, x, w, bias, y, residual);
 
   int tile = d->tile ? d->tile : pick_tile(d, residual == nullptr);  // tile 22 stores no residual
   YCX_CHECK_SUPPORTED(tile > 0 && tile < kNumTiles);
+  YCX_CHECK_SUPPORTED(!d->in_pool || tile == 16 || tile == 18 || tile == 25);
   const TileInfo& t = kTiles[tile];
   YCX_CHECK_SUPPORTED(d->cin % t.bk == 0 && d->cout_pad % t.bm == 0);
   YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_FP8) == (tile >= 34 && tile <= 37));
@@ -3098,6 +3166,7 @@ extern "C" ycx_status ycx_conv2d_head(const ycx_conv_desc* d, const ycx_head_des
   const bool f8 = d->dtype == YCX_DT_FP8;
   YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_BF16 || f8) && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0);
   YCX_CHECK_SUPPORTED(d->act == YCX_ACT_NONE && d->out_layout == YCX_OUT_NCHW_F32 && d->cout_pad == 256);
+  YCX_CHECK_SUPPORTED(!d->in_pool);
   YCX_CHECK_SUPPORTED(f8 ? (d->in_c_off % 16 == 0 && d->in_c_stride % 16 == 0)
                          : (d->in_c_off % 8 == 0 && d->in_c_stride % 8 == 0));
   YCX_CHECK_SUPPORTED((long long)d->n * d->h * d->w * d->in_c_stride * 2 < (1LL << 31));
@@ -3120,7 +3189,7 @@ extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, cons
                       d->out_c_stride % 8 == 0 && d->out_c_off + d->cout <= d->out_c_stride);
   YCX_CHECK_SUPPORTED(d->out_layout == YCX_OUT_NHWC || d->out_layout == YCX_OUT_NHWC_UP2);
   YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
-  YCX_CHECK_SUPPORTED((long long)d->n * d->ho * d->wo < (1LL << 31));
+  YCX_CHECK_SUPPORTED((long long)d->n * d->ho * d->wo < (1LL << 31) && !d->in_pool);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ConvArgs a = make_args(d, x, w, bias, y, nullptr);
   a.Ktot = d->kh * d->kw * d->cin;  // fp32 stem weights: no fp8 row padding

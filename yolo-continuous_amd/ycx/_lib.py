@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see above)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("YCX_LIB", os.path.join(_HERE, "libycx_hip.so"))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # ---- enums (ycx.h) ----
 YCX_OK, YCX_ERR_BAD_ARG, YCX_ERR_UNSUPPORTED, YCX_ERR_LAUNCH, YCX_ERR_CAPACITY = 0, 1, 2, 3, 4
@@ -36,7 +36,7 @@ class ConvDesc(ctypes.Structure):
         "ho", "wo", "cout", "cout_pad", "out_c_off", "out_c_stride",
         "kh", "kw", "stride", "pad", "act")] + [("leaky_slope", ctypes.c_float)] + [
         (n, _i32) for n in ("dtype", "out_layout", "res_c_off", "res_c_stride", "tile")] + [
-        ("out_scale", ctypes.c_float), ("res_scale", ctypes.c_float)]
+        ("out_scale", ctypes.c_float), ("res_scale", ctypes.c_float), ("in_pool", _i32)]
 
 
 class PoolDesc(ctypes.Structure):

@@ -438,7 +438,8 @@ def pack_fp8_weights(wp):
 class Engine:
     """A compiled plan bound to device memory for one (input shape, device, precision)."""
 
-    def __init__(self, model, shape, device, precision='bf16', fuse_stem2=True, fp8_amax=None, prepacked=None):
+    def __init__(self, model, shape, device, precision='bf16', fuse_stem2=True, fp8_amax=None, prepacked=None,
+                 fuse_pool=True):
         if device.type != 'cuda':
             raise RuntimeError("ycx: the HIP path needs the model input on a ROCm device (tensor.to('cuda')); "
                                "there is no CPU path")
@@ -447,6 +448,7 @@ class Engine:
         self.dtype = {'bf16': torch.bfloat16, 'f32': torch.float32, 'fp8': torch.float8_e4m3fn}[precision]
         self.dt = {'bf16': L.DT_BF16, 'f32': L.DT_F32, 'fp8': L.DT_FP8}[precision]
         self.fuse_stem2 = fuse_stem2
+        self.fuse_pool = fuse_pool  # False: every pool writes its map (fp8 calibration reads them all)
         self.prepacked = prepacked  # {'p<i>': packed tensor} from ycx.prepack (skips folding / packing)
         self.graph_exec = None
         self.graph, self.out_vals, self.is_list = self.plan.graph, self.plan.out_vals, self.plan.is_list
@@ -555,6 +557,8 @@ class Engine:
         cascades = self._pool_cascades()
         for c in cascades.values():
             fused.update(id(nd) for nd in c[1:])
+        pooled = self._pool_convs()  # {id(conv): pool node} (the pool runs inside the conv)
+        fused.update(id(nd) for nd in pooled.values())
         for node in self.graph.nodes:
             k = node.kind
             if id(node) in fused:
@@ -562,7 +566,7 @@ class Engine:
             if id(node) in pairs:
                 ops.append(self._stem2_op(node, pairs[id(node)]))
             elif k in ('conv', 'stem'):
-                ops.append(self._conv_op(node))
+                ops.append(self._conv_op(node, pool=pooled.get(id(node))))
             elif k == 'pool':
                 ops.append(self._pool_op(node, levels=len(cascades.get(id(node), [node]))))
             elif k == 'up':  # an unfused upsample may write a slice of a concat buffer
@@ -591,9 +595,10 @@ class Engine:
             return None
         return v.buf.tensor.data_ptr()
 
-    def _conv_parts(self, node, bf16_weights=False):
+    def _conv_parts(self, node, bf16_weights=False, pool=None):
         """Packed weights/bias (kept alive in self.params) and the descriptor of a conv/stem node.
-        bf16_weights: bf16 packing whatever the plan dtype (the fp8 stem2 pair computes in bf16)."""
+        bf16_weights: bf16 packing whatever the plan dtype (the fp8 stem2 pair computes in bf16).
+        pool: the k2 s2 pool node feeding this 1x1 conv, fused into it (``_pool_convs``)."""
         p, x, out = node.p, node.inputs[0], node.out
         w64, b64 = p['w'], p['b']
         cout, cin, k = int(w64.shape[0]), int(w64.shape[1]), p['k']
@@ -639,6 +644,9 @@ class Engine:
             d.in_c_off, d.in_c_stride = 0, x.c
         else:
             d.in_c_off, d.in_c_stride = x.coff, x.buf.c
+        if pool is not None:  # read the pool's (2h, 2w) input map instead of its output
+            src = pool.inputs[0]
+            d.in_c_off, d.in_c_stride, d.in_pool = src.coff, src.buf.c, 1
         d.ho, d.wo, d.cout, d.cout_pad = p['ho'], p['wo'], cout, cpad
         d.kh = d.kw = k
         d.stride, d.pad, d.act, d.leaky_slope = p['s'], p['p'], p['act'], p['slope']
@@ -657,15 +665,15 @@ class Engine:
         self.conv_flops += flops
         return d, wt, bt, flops, (x.n, x.h, x.w, cin, cout, k, p['s'])
 
-    def _conv_op(self, node):
+    def _conv_op(self, node, pool=None):
         x, out, r = node.inputs[0], node.out, node.p['residual']
         stem = node.kind == 'stem'
-        d, wt, bt, flops, shape = self._conv_parts(node)
+        d, wt, bt, flops, shape = self._conv_parts(node, pool=pool)
         op = L.Op()
         op.kind = L.OP_STEM if stem else L.OP_CONV
         op.d.conv = d
         idx = len(self.op_info)
-        op.in_ = self._val_ptr(x, idx, 'in_')
+        op.in_ = self._val_ptr(x if pool is None else pool.inputs[0], idx, 'in_')
         op.weight, op.bias = wt.data_ptr(), bt.data_ptr()
         op.out = self._val_ptr(out, idx, 'out')
         op.residual = r.buf.tensor.data_ptr() if r is not None else None
@@ -676,6 +684,8 @@ class Engine:
                     tile = d.tile = t
                     break
         name = 'stem' if stem else L.lib.ycx_conv_tile_name(tile).decode()
+        if pool is not None:
+            name += '+maxpool_k2s2'
         self.op_info.append(dict(kind=node.kind, name=name, flops=flops, shape=shape, parts=node.p.get('parts', 1)))
         return op
 
@@ -721,6 +731,34 @@ class Engine:
             if len(chain) > 1:
                 out[id(a)] = chain
                 used.update(id(nd) for nd in chain)
+        return out
+
+    def _pool_convs(self):
+        """MP's k2 s2 pools (nets/common.py:25-31) whose map is read only by one 1x1 / s1
+        conv: the conv pools its operand while staging it (ycx_conv_desc.in_pool, bf16
+        plans), so the pooled map is never written. yolov7: all five MP pools.
+        Returns {id(conv node): pool node}."""
+        if self.dt != L.DT_BF16 or not self.fuse_pool or os.environ.get('YCX_NO_POOL_FUSE'):
+            return {}
+        out = {}
+        for nd in self.graph.nodes:
+            if nd.kind != 'pool':
+                continue
+            p, x, v = nd.p, nd.inputs[0], nd.out
+            if not (p['k'] == 2 and p['s'] == 2 and p['p'] == 0 and x.h == 2 * v.h and x.w == 2 * v.w):
+                continue
+            if x.role != 'act' or v.role != 'act' or len(v.consumers) != 1 or x.coff % 8 or x.buf.c % 8:
+                continue
+            c = v.consumers[0]
+            q = c.p
+            if c.kind != 'conv' or c.inputs[0] is not v or not (q['k'] == 1 and q['s'] == 1 and q['p'] == 0):
+                continue
+            cin, cout = int(q['w'].shape[1]), int(q['w'].shape[0])
+            if cin % 64 or self._cout_pad(cout) % 64 or q['layout'] == L.OUT_NCHW_F32:
+                continue
+            if x.n * x.h * x.w * x.buf.c * 2 >= 1 << 31:
+                continue
+            out[id(c)] = nd
         return out
 
     def _pool_op(self, node, levels=1):
