@@ -5,9 +5,10 @@ One step = one batch through the whole hot path, device resident:
   -> fused decode + filter (ycx_decode_filter) -> sort + per-class NMS (ycx_sort_nms)
   -> (N > 1) one RCCL all_gather of the padded detections over xGMI.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch B]
 For N > 1 launch with torch.distributed.run (one process per GPU); images are
-sharded by rank (weak scaling: 32 images per GPU per step).
+sharded by rank (weak scaling: 32 images per GPU per step; --global-batch B:
+strong scaling, B images per step split over the ranks, "scaling": "strong").
 
 Prints ONE JSON line (rank 0) with images/s for the whole job, p50 step
 latency, the dominant kernel's roofline, and the CPU-oracle baseline.
@@ -41,7 +42,10 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling (SURVEY.md 8(e)): this many images per step over all ranks, "
+                         "split evenly (32 over 1/2/4/8 GPUs = 32/16/8/4 each); overrides --batch")
     ap.add_argument("--size", type=int, default=640)
     ap.add_argument("--net", default="yolov7")
     ap.add_argument("--nc", type=int, default=80)
@@ -90,7 +94,7 @@ def roofline(det, steps, precision):
     per = {}
     per_op = [0.0] * n
     for _ in range(steps):
-        eng.run_static(events=evs)
+        det.forward(events=evs)  # counts reset first: the fused heads append this forward's candidates
         torch.cuda.synchronize()
         for i, info in enumerate(eng.op_info):
             ms = evs[i].elapsed_time(evs[i + 1])
@@ -334,6 +338,10 @@ def main():
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     dist_on = world > 1 or args.dist  # --dist: the N > 1 code path (RCCL gather) on a single rank
+    if args.global_batch:
+        if args.global_batch % world:
+            raise SystemExit(f"--global-batch {args.global_batch} does not split over {world} ranks")
+        args.batch = args.global_batch // world
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
@@ -419,7 +427,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "p50_ms": round(statistics.median(lat), 4), "p90_ms": round(sorted(lat)[int(0.9 * (len(lat) - 1))], 4),
             "p50_ms_unloaded": round(statistics.median(lat1), 4) if lat1 else None,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "higher_is_better": True, "scaling": "strong" if args.global_batch else "weak", "vs_baseline": None,
+            "dtype": args.precision,
             "data": "synthetic U[0,1) images, seeded synthetic weights (no checkpoint exists)",
             "config": {"workload": f"{args.net} COCO-{args.nc} {args.size}x{args.size}, {args.batch} images per GPU "
                                    f"per step: forward + decode + NMS (+ all-gather)",

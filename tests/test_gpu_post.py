@@ -378,6 +378,7 @@ def test_detector_graph_matches_eager(device):
     x = synthetic_images(*shape, seed=4).to(device)
     g = Detector(m, shape, device, ANCHORS, MASK, use_graph=True)
     d1, k1, c1 = [t.clone() for t in g(x)]   # HIP graph replay + post
+    g.counts.zero_()                          # the fused heads append this forward's candidates
     g.engine.run_static()                     # eager ycx_run_ops on the same static buffers
     d2, k2, c2 = [t.clone() for t in g.post()]
     torch.cuda.synchronize()

@@ -590,7 +590,7 @@ __device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const fl
         int slot = s_cnt[32 + k] + __popcll((k ? q1 : q0) & ((1ull << lane) - 1ull));
         for (int w = 0; w < wid; ++w) slot += s_cnt[2 * w + k];
         hd.cand[(size_t)n * h.rows_total + cd.row] = cd;
-        hd.rows_out[(size_t)n * h.rows_total + slot] = cd.row;
+        if (slot < h.rows_total) hd.rows_out[(size_t)n * h.rows_total + slot] = cd.row;  // counts not reset: no overrun
       }
       __syncthreads();  // s_cnt is reused by the next pass
       continue;
@@ -608,7 +608,7 @@ __device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const fl
       if (mine) {
         const int slot = base + __popcll(q & ((1ull << lane) - 1ull));
         hd.cand[(size_t)nl * h.rows_total + cd.row] = cd;
-        hd.rows_out[(size_t)nl * h.rows_total + slot] = cd.row;
+        if (slot < h.rows_total) hd.rows_out[(size_t)nl * h.rows_total + slot] = cd.row;
       }
       rem &= ~q;
     }

@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(256) filter_decoded_kernel(ycx_filter_desc d, 
   const int slot = wave_append(pass, counts + n);
   if (pass) {
     cand[(size_t)n * d.rows + r] = c;
-    rows_out[(size_t)n * d.rows + slot] = r;
+    if (slot < d.rows) rows_out[(size_t)n * d.rows + slot] = r;  // counts not reset by the caller: no overrun
   }
 }
 
@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(256) decode_filter_kernel(DecodeFilterArgs a, 
   const int slot = wave_append(pass, counts + n);
   if (pass) {
     cand[(size_t)n * d.rows_total + r] = c;
-    rows_out[(size_t)n * d.rows_total + slot] = r;
+    if (slot < d.rows_total) rows_out[(size_t)n * d.rows_total + slot] = r;  // (counts not reset: no overrun)
   }
 }
 
@@ -407,7 +407,8 @@ __global__ void __launch_bounds__(256) decode_filter4_kernel(DecodeFilterArgs a,
   for (int i = 0; i < 4; ++i) {
     if (pass[i]) {
       cand[(size_t)n * d.rows_total + r0 + i] = c[i];
-      rows_out[(size_t)n * d.rows_total + slot++] = r0 + i;
+      if (slot < d.rows_total) rows_out[(size_t)n * d.rows_total + slot] = r0 + i;
+      ++slot;
     }
   }
 }
