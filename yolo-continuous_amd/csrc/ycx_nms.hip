@@ -56,8 +56,11 @@ constexpr int kMaxRows = 131072;  // rows (candidates) per image
 #endif
 constexpr int kBigBlocks = YCX_NMS_BIG_BLOCKS;   // nms_big grid (task-strided)
 constexpr int kSlots = 16;        // highest-ranked suppressors cached per box
-constexpr int kLevels = 7;        // size octaves: level L holds max(w, h) < 2^-L of the class extent
-constexpr int kGridCells = 5461;  // sum_{L < 7} 4^L
+#ifndef YCX_NMS_LEVELS
+#define YCX_NMS_LEVELS 7
+#endif
+constexpr int kLevels = YCX_NMS_LEVELS;  // size octaves: level L holds max(w, h) < 2^-L of the class extent
+constexpr int kGridCells = ((1 << (2 * kLevels)) - 1) / 3;  // sum_{L < kLevels} 4^L
 constexpr int kWild = kGridCells; // one extra cell: boxes without a finite positive size
 constexpr int kCells = kGridCells + 1;
 
@@ -717,7 +720,8 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
                                                     Thr thr, float t_lo, float inv_t, int all_pairs) {
   constexpr int kLdsBytes = kBigLds;
   constexpr int kLdsCellBytes = ((kCells * 4) + 255) & ~255;
-  static_assert(kLdsBytes >= 16 * kBigThreads * 8, "LDS keys of the register sorts (E <= 16)");
+  // register sorts exchange through LDS when the keys fit (Pn <= kLdsBytes / 8), else the workspace
+  static_assert(kLdsBytes >= 8 * kBigThreads * 8 && kLdsBytes >= ((kCells * 4 + 255) & ~255) + 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
   __shared__ int s_lv[kLevels][5];
   __shared__ int s_ext[4];
