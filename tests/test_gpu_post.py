@@ -385,6 +385,30 @@ def test_detector_graph_matches_eager(device):
     assert torch.equal(c1, c2) and torch.equal(k1, k2) and torch.equal(d1, d2)
 
 
+def test_fused_append_bounded_without_reset(device):
+    """A caller that replays the fused forward without resetting the candidate counts
+    keeps appending past rows_total: the counts grow, the row list stays in bounds
+    (the writes past it are dropped) and a reset restores the exact result."""
+    m, _ = make_model('yolov7-tiny', 1, 0, 'bf16')
+    m.to(device)
+    shape = (2, 3, 256, 256)
+    x = synthetic_images(*shape, seed=4).to(device)
+    g = Detector(m, shape, device, ANCHORS, MASK, use_graph=False)
+    assert g.fused
+    d1, k1, c1 = [t.clone() for t in g(x)]
+    n1 = g.counts.clone()
+    guard = torch.full((1 << 16,), 7, dtype=torch.int32, device=device)  # allocated after the row list
+    reps = g.rows // max(1, int(n1.min())) + 2  # enough replays to pass rows_total
+    assert int(n1.min()) > 0 and reps <= 64, (n1, g.rows)
+    for _ in range(reps):
+        g.engine.run_static()
+    torch.cuda.synchronize()
+    assert bool((g.counts > g.rows).all()) and bool((guard == 7).all())
+    d2, k2, c2 = [t.clone() for t in g(x)]  # forward() resets the counts
+    torch.cuda.synchronize()
+    assert torch.equal(g.counts, n1) and torch.equal(k1, k2) and torch.equal(c1, c2) and torch.equal(d1, d2)
+
+
 def test_pipelined_detector_matches_serial(device):
     """Two slots on two streams, five batches in flight back to back: every
     batch's detections equal the single-stream Detector's on the same images."""
