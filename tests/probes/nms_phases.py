@@ -46,6 +46,12 @@ def main():
           f"suppressor pairs/task {buf[10] / nt:.0f}")
     cnt = det.counts.cpu()
     print("candidates/img", cnt.float().mean().item())
+    ws = det.ws.view(torch.int32).cpu()  # header (ntasks) then the task table {img, cls, off, S} at byte 256
+    nt = int(ws[0])
+    S = ws[64:64 + 4 * nt].view(nt, 4)[:, 3].sort().values
+    lds_cap = (159744 - 22016 - 32) // 19
+    print(f"big classes {nt}: S min {int(S[0])} median {int(S[nt // 2])} max {int(S[-1])}, "
+          f"{int((S > lds_cap).sum())} over the LDS capacity {lds_cap}")
 
 
 if __name__ == "__main__":
