@@ -40,8 +40,10 @@ ROUND = "r02"  # profiles/<ROUND>/: rocprofv3 summaries of this round's bench co
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 100 timed steps (≈ 0.5 s): with three batches in flight the pipeline fill and the final
+    # drain inside the timed region cost ≈ 4 % of a 20-step run
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=32, help="images per GPU per step (weak scaling)")
     ap.add_argument("--global-batch", type=int, default=0,
                     help="strong scaling (SURVEY.md 8(e)): this many images per step over all ranks, "
