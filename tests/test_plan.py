@@ -51,6 +51,32 @@ def test_plan_yolov7_layout():
     assert all(nd.p['k'] in (2, 5) for nd in plan.graph.nodes if nd.kind == 'pool')
 
 
+def test_pool_fusion_pass_finds_the_mp_blocks():
+    """The engine's MP-pool fusion pass (host logic, no GPU): every yolov7 k2 s2 pool feeds
+    exactly one 1x1 / s1 conv and is fused into it; in yolov7-tiny only pools read by a lone 1x1
+    fuse; fp8 / f32 plans and fuse_pool=False keep every pool."""
+    from ycx import _lib as L
+    from ycx.engine import Engine
+
+    def pairs(net, nc, dt=L.DT_BF16, fuse=True):
+        plan = Plan(Model(cvt_cfg(net), ANCHORS, nc), (2, 3, 640, 640))
+        eng = Engine.__new__(Engine)  # the pass reads the plan graph and the plan dtype only
+        eng.graph, eng.dt, eng.fuse_pool = plan.graph, dt, fuse
+        return eng._pool_convs()
+
+    got = pairs('yolov7', 80)
+    assert len(got) == 5
+    for pool in got.values():
+        p = pool.p
+        assert (p['k'], p['s'], p['p']) == (2, 2, 0) and pool.inputs[0].h == 2 * pool.out.h
+        (conv,) = pool.out.consumers
+        assert conv.kind == 'conv' and (conv.p['k'], conv.p['s'], conv.p['p']) == (1, 1, 0)
+    assert pairs('yolov7', 80, dt=L.DT_FP8) == {} and pairs('yolov7', 80, dt=L.DT_F32) == {}
+    assert pairs('yolov7', 80, fuse=False) == {}
+    for pool in pairs('yolov7-tiny', 1).values():
+        assert pool.out.consumers[0].p['k'] == 1
+
+
 def test_fold_bn_and_repconv_exact():
     torch.manual_seed(0)
     for c1, c2, s in ((16, 32, 1), (32, 32, 1), (16, 16, 2)):
