@@ -6,9 +6,11 @@ One step = one batch through the whole hot path, device resident:
   -> (N > 1) one RCCL all_gather of the padded detections over xGMI.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch B]
-For N > 1 launch with torch.distributed.run (one process per GPU); images are
-sharded by rank (weak scaling: 32 images per GPU per step; --global-batch B:
-strong scaling, B images per step split over the ranks, "scaling": "strong").
+--gpus N > 1 starts N rank processes by itself (one per GPU, before any GPU
+call in the parent); a launch under torch.distributed.run (WORLD_SIZE set) is
+used as is. Images are sharded by rank (weak scaling: 32 images per GPU per
+step; --global-batch B: strong scaling, B images per step split over the ranks,
+"scaling": "strong").
 
 Prints ONE JSON line (rank 0) with images/s for the whole job, p50 step
 latency, the dominant kernel's roofline, and the CPU-oracle baseline.
@@ -34,7 +36,18 @@ ANCHORS = [[12, 16, 19, 36, 40, 28], [36, 75, 76, 55, 72, 146], [142, 110, 192, 
 MASK = [[6, 7, 8], [3, 4, 5], [0, 1, 2]]
 METRIC = "images/sec (whole node) + p50 end-to-end latency, 640×640 bs=32, 1/2/4/8 MI355X"
 PEAK = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
-ROUND = "r02"  # profiles/<ROUND>/: rocprofv3 summaries of this round's bench command
+
+
+def _current_round():
+    """profiles/<round>/ of the newest round that holds a PMC traffic summary
+    (``--round`` overrides): roofline.traffic is read from there."""
+    base = os.path.join(REPO, "profiles")
+    try:
+        rounds = sorted(d for d in os.listdir(base)
+                        if d[:1] == "r" and d[1:].isdigit() and os.path.isfile(os.path.join(base, d, "traffic.json")))
+    except OSError:
+        rounds = []
+    return rounds[-1] if rounds else None
 
 
 def parse(argv=None):
@@ -81,6 +94,11 @@ def parse(argv=None):
     ap.add_argument("--obj-shift", type=float, default=-3.0, help="--post-micro: objectness logit shift")
     ap.add_argument("--diag-forward-only", action="store_true",
                     help="DIAGNOSTIC (not the metric): time the forwards alone, no decode / NMS")
+    ap.add_argument("--round", default=None,
+                    help="profiles/<round>/traffic.json for roofline.traffic (default: the newest round that has one)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: every rank joins a gloo process group, all-gathers "
+                         "fabricated padded detections and rank 0 prints one JSON line (no GPU legs)")
     return ap.parse_args(argv)
 
 
@@ -227,10 +245,12 @@ def setup(args, dev, rank=0, use_graph=None, pipeline=False):
     return model, det, sd, cfg, shape
 
 
-def pmc_traffic(kernel, shape):
-    """HBM bytes per launch of ``kernel`` from this round's PMC passes
-    (tools/pmc_traffic.py -> profiles/<ROUND>/traffic.json), or None."""
-    path = os.path.join(REPO, "profiles", ROUND, "traffic.json")
+def pmc_traffic(kernel, shape, rnd):
+    """HBM bytes per launch of ``kernel`` from round ``rnd``'s PMC passes
+    (tools/pmc_traffic.py -> profiles/<rnd>/traffic.json), or None."""
+    if rnd is None:
+        return None
+    path = os.path.join(REPO, "profiles", rnd, "traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
@@ -326,17 +346,96 @@ def post_micro(args, dev):
     print(json.dumps(out), flush=True)
 
 
-def main():
-    args = parse()
+def launch_ranks(args, argv):
+    """``--gpus N`` (N > 1) without WORLD_SIZE in the environment: start N rank
+    processes of this same script, one per GPU (RANK = LOCAL_RANK = i,
+    WORLD_SIZE = N, rendezvous on 127.0.0.1 at a free port), and return the
+    worst exit code. The parent never touches the GPU (it only counts devices,
+    which does not initialise HIP on this image) and starts the ranks as child
+    processes, never by exec. If a rank fails the others are stopped instead
+    of waiting at a barrier forever."""
+    import socket
+    import subprocess
+    if not args.dry_run:
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but only {have} GPU(s) are visible")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   YCX_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    codes = [None] * len(procs)
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+        if any(c not in (None, 0) for c in codes):
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    try:
+                        codes[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[i] = p.wait()
+            break
+        time.sleep(0.05)
+    return max((abs(c) for c in codes), default=0)
+
+
+def dry_run(args, world, rank):
+    """The N-rank launcher path without a GPU: a gloo process group, the bench's
+    one collective on fabricated padded detections [batch, max_det, 7] (+ counts,
+    keep rows), max-over-ranks timing; rank 0 prints one JSON line."""
+    from ycx.dist import gather_detections
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = args.batch
+        dets = torch.full((n, args.max_det, 7), float(rank))
+        keep = torch.full((n, args.max_det), rank, dtype=torch.int32)
+        kc = torch.full((n,), rank, dtype=torch.int32)
+        dist.barrier()
+        t0 = time.perf_counter()
+        g_dets, g_kc, g_keep = gather_detections(dets, kc, keep)
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ok = bool(torch.equal(g_kc, torch.arange(world, dtype=torch.int32).repeat_interleave(n)))
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": args.gpus, "rccl_world_size": dist.get_world_size(),
+                              "backend": dist.get_backend(), "gathered_dets": list(g_dets.shape),
+                              "gathered_keep": list(g_keep.shape), "rank_major_order": ok,
+                              "gather_s": float(t.item())}), flush=True)
+        if not ok:
+            raise SystemExit("dry run: gathered counts are not in rank-major order")
+    finally:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
     if args.post_micro:
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
         return post_micro(args, dev)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    rnd = args.round or _current_round()
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     dist_on = world > 1 or args.dist  # --dist: the N > 1 code path (RCCL gather) on a single rank
@@ -445,12 +544,14 @@ def main():
                                               (world * peak * 1e12), 4),
             "roofline": {"bound": "mfma", "kernel": rl['kernel'], "achieved": round(rl['achieved'], 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(rl['achieved'] / peak, 4),
-                         "traffic": pmc_traffic(rl['kernel'], shape), "traffic_unit": "bytes/launch (HBM, PMC)",
+                         "traffic": pmc_traffic(rl['kernel'], shape, rnd),
+                         "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_round": rnd,
                          "avg_launch_ms": round(rl['avg_launch_ms'], 5),
                          "flops_per_launch": int(rl['flops_per_launch']),
                          "all_conv_tflops": round(rl['all_conv_tflops'], 2),
                          "forward_kernel_ms": round(rl['forward_kernel_ms'], 4)},
             "cpu_baseline": cpu,
+            "rccl_world_size": dist.get_world_size() if dist_on else 1,
             "detections_last_step": int(kc.sum().item()),
         }
         print(json.dumps(out), flush=True)
@@ -463,4 +564,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -105,3 +105,24 @@ def test_to_output_list_truncation_is_explicit():
         warnings.simplefilter("error")
         ok = to_output_list(dets, torch.tensor([1, 4, 0], dtype=torch.int32))
     assert not ok.any_truncated and ok[1].shape == (4, 7)
+
+
+def test_bench_launches_n_ranks_itself():
+    """``python bench.py --gpus 2`` (no torchrun, no WORLD_SIZE)
+    starts its own 2 rank processes; --dry-run takes the launcher path with a
+    gloo group instead of the GPU legs. Exactly one JSON line (rank 0) comes out,
+    and it reports the process group's world size."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run", "--batch", "4"],
+                       env=env, capture_output=True, text=True, timeout=180, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["rccl_world_size"] == 2 and out["n_gpus"] == 2 and out["rank_major_order"]
+    assert out["gathered_dets"] == [8, 300, 7] and out["gathered_keep"] == [8, 300]

@@ -17,14 +17,16 @@ import torch
 
 from helpers import ANCHORS, MASK, fused_keep_report, make_model, rel_err
 from oracle import ref_forward
-from ycx.detect import ConcurrentDetector, Detector
+from ycx.detect import ConcurrentDetector, Detector, device_nms
 from ycx.utils.helper_io import cvt_cfg
 from ycx.utils.synth import synthetic_images
 
 pytestmark = pytest.mark.gpu
 A = np.asarray(ANCHORS).reshape(-1, 2)
 C2_BAR, C5_BAR = 1e-2, 0.10   # heads: max |gpu - oracle| / max |oracle| (bf16, fp8 e4m3); measured r02: 0.0045, 0.088
-KEEP_FLIPS_PIN = {'c2': 6, 'c5': 4, 'c4': 12}   # measured on MI355X: 3/0, 0/0, 6
+# end-to-end keep-set differences over the FULL survivor lists (images 0 / n-1), all from
+# sigmoid/exp ulps in the device decode (nms_exact holds); provisional until measured
+KEEP_FLIPS_PIN = {'c2': 60, 'c5': 60, 'c4': 12}
 
 
 @pytest.fixture(scope='module')
@@ -87,8 +89,18 @@ def _bench_config(device, precision, bs, seed):
     for info in det.engine.op_info:
         tiles[info['name']] = tiles.get(info['name'], 0) + 1
     print(f"\n{precision} bs={bs} plan tiles: {tiles}")
+    # the bench slot keeps max_det = 300 rows per image; for the parity check the same
+    # device candidates go through ycx_sort_nms again with room for every survivor
+    # (max_det = rows_total), and the bench's 300 rows must be that list's prefix
+    rows_total = det.cand.shape[1]
+    _, keep_full, kc_full = device_nms(det.cand, det.cand_rows, det.counts, 80, 0.3, rows_total)
+    torch.cuda.synchronize()
+    keep_full, kc_full = keep_full.cpu(), kc_full.cpu()
+    keep300, kc300 = det.keep.cpu(), det.kc.cpu()
+    assert torch.equal(kc_full, kc300), "the uncapped survivor counts depend on max_det"
+    assert torch.equal(keep_full[:, :300], keep300), "the bench's 300 rows are not the full list's prefix"
     out = dict(heads=[h.cpu() for h in det.heads], cand=det.cand.cpu(), cand_rows=det.cand_rows.cpu(),
-               counts=det.counts.cpu(), keep=det.keep.cpu(), kc=det.kc.cpu(), tiles=tiles, bs=bs)
+               counts=det.counts.cpu(), keep=keep_full, kc=kc_full, tiles=tiles, bs=bs, rows_total=rows_total)
     ref = ref_forward.build(cvt_cfg('yolov7'), ANCHORS, 80, sd)(x[[0, bs - 1]])
     out['ref'] = ref
     del cd, det
@@ -118,9 +130,11 @@ def _check_heads(cfg, bar):
 
 
 def _check_keep(cfg, name):
+    """Every survivor's keep row of images 0 and n-1 (not the first 300)."""
     for b in (0, cfg['bs'] - 1):
+        assert int(cfg['kc'][b]) > 300  # the bench load: thousands of survivors per image
         rep = fused_keep_report(cfg['cand'], cfg['cand_rows'], cfg['counts'], cfg['keep'], cfg['kc'], b,
-                                [h[b] for h in cfg['heads']], 80, 0.3, 0.3, 640, 300)
+                                [h[b] for h in cfg['heads']], 80, 0.3, 0.3, 640, cfg['rows_total'])
         print(f"\n{name} image {b}: {rep}")
         assert rep['cls_same'], "class ids differ on common candidates"
         assert rep['box_maxdiff'] <= 2e-6, rep          # device decode vs oracle decode, normalised xyxy

@@ -159,3 +159,50 @@ def test_forward_rejects_cpu_and_training():
     m.train()
     with pytest.raises(RuntimeError, match='inference-only'):
         m(torch.zeros(1, 3, 64, 64))
+
+
+@pytest.mark.parametrize('hw,cascade', [(24, True), (48, False)])
+def test_sppcspc_pool_cascade_size_limit(device, manifest, hw, cascade):
+    """the one-launch 5/9/13 cascade keeps two copies of the map's plane in
+    64 KB of LDS. A 48^2 map (2304 pixels, 64 channels) does not fit; the plan must fall
+    back to three pool launches (not fail in run_ops), and both forms match the oracle."""
+    from ycx.engine import cascade_fits
+    e = manifest['g1']['sppcspc']
+    assert cascade_fits(hw, hw, 64, 2) == cascade
+    m, sd = make_model(e['cfg'], e['nc'], e['w_seed'], 'bf16')
+    m.to(device)
+    x = synthetic_images(1, 3, hw, hw, seed=21)
+    eng = m.engine_for(x.shape, device)
+    pools = [i['name'] for i in eng.op_info if i['kind'] == 'pool']
+    assert pools == (['maxpool_k5s1_cascade3'] if cascade else ['maxpool_k5s1'] * 3), pools
+    y = m(x.to(device))
+    ref = ref_forward.build(e['cfg'], ANCHORS, e['nc'], sd)(x)
+    for o, r in zip(_outs(y), _outs(ref)):
+        assert rel_err(o.cpu(), r) < BF16_TOL
+
+
+def test_detector_close_releases_its_engine(device):
+    """every Detector owns a private engine; close() (or collecting the
+    Detector) removes it from the model's engine table, so repeated Detectors do
+    not accumulate activation buffers."""
+    import gc
+    from ycx.detect import ConcurrentDetector, Detector
+    m, _ = make_model('yolov7-tiny', 1, 0, 'bf16')
+    m.to(device)
+    shape = (1, 3, 64, 64)
+    base = len(m._engines)
+    det = Detector(m, shape, device, ANCHORS, [[6, 7, 8], [3, 4, 5], [0, 1, 2]], use_graph=True)
+    det(torch.zeros(shape, device=device))
+    torch.cuda.synchronize()
+    assert len(m._engines) == base + 1
+    det.close()
+    assert len(m._engines) == base
+    for _ in range(3):  # dropped without close(): the finaliser releases the engine
+        Detector(m, shape, device, ANCHORS, [[6, 7, 8], [3, 4, 5], [0, 1, 2]], use_graph=False)
+        gc.collect()
+    assert len(m._engines) == base
+    cd = ConcurrentDetector(m, shape, device, ANCHORS, [[6, 7, 8], [3, 4, 5], [0, 1, 2]], depth=3)
+    assert len(m._engines) == base + 3
+    cd.submit(torch.zeros(shape, device=device))
+    cd.close()
+    assert len(m._engines) == base

@@ -165,7 +165,7 @@ def test_device_post_dense_class_scan(device, scalar, monkeypatch):
         hd[:, :, 4] = 6.0
         flat = hd.permute(0, 1, 3, 4, 2).reshape(-1, 5 + nc)   # view: rows x channels
         for r in rng.choice(flat.shape[0], size=flat.shape[0] // 2, replace=False):
-            kind = int(rng.integers(8))
+            kind = int(rng.integers(9))
             ks = rng.choice(nc, size=3, replace=False)
             if kind == 0:
                 flat[r, 5 + ks] = torch.tensor([18.0, 25.0, 40.0])          # saturated: all 1.0
@@ -186,8 +186,13 @@ def test_device_post_dense_class_scan(device, scalar, monkeypatch):
                 flat[r, 5 + ks[1]] = 9.0
             elif kind == 6:
                 flat[r, 5] = float('nan')                                    # class 0 NaN sticks
-            else:
+            elif kind == 7:
                 flat[r, 5 + ks] = torch.tensor([16.5, 16.6, 16.7])           # edge of saturation
+            else:   # every sigmoid 0: -inf before the largest logit ties it (the scan keeps class 0)
+                j = int(ks[0]) % 8 + 1
+                flat[r, 5:5 + j] = float('-inf')
+                flat[r, 5 + j] = -200.0
+                flat[r, 5 + j + 1:] = -250.0
         hd.copy_(flat.reshape(hd.shape[0], hd.shape[1], hd.shape[3], hd.shape[4], 5 + nc).permute(0, 1, 4, 2, 3))
     heads = [hd.reshape(bs, 3 * (5 + nc), h, w).contiguous() for hd, (h, w) in zip(heads, shapes)]
     dh = [h.to(device) for h in heads]

@@ -176,3 +176,13 @@ def test_iauxdetect_lowers_main_heads_only(manifest):
     assert len(convs) == 4 + 3  # stem + 3 backbone convs + 3 main heads (aux layers 4-6 and m2 dropped)
     assert [v.c for v in plan.out_vals] == [3 * (e['nc'] + 5)] * 3
     assert [(v.h, v.w) for v in plan.out_vals] == [(12, 12), (6, 6), (3, 3)]
+
+
+def test_cascade_fits_mirrors_the_kernel_limit():
+    """ycx_maxpool levels > 1: two planes of a 16-byte-multiple channel slice in 64 KB."""
+    from ycx.engine import cascade_fits
+    assert cascade_fits(20, 20, 512, 2) and cascade_fits(40, 40, 256, 2)     # yolov7 at 640 / 1280
+    assert cascade_fits(45, 45, 512, 2) and not cascade_fits(46, 46, 512, 2)  # 2025 / 2116 pixels, bf16
+    assert not cascade_fits(40, 60, 512, 2)                                   # 1280x1920 input
+    assert cascade_fits(45, 45, 512, 1) and not cascade_fits(46, 46, 512, 1)  # e4m3: a 16-channel slice
+    assert not cascade_fits(8, 8, 4, 2)                                       # slice below 16 bytes

@@ -769,6 +769,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
       if (b_base[i] < 0) v = bf16x8{};
       *reinterpret_cast<bf16x8*>(base + (wid + NW * i) * 1024 + lane * 16) = v;
     }
+    // the next raw s_barrier does not wait for LDS stores by itself (gfx950 back-off
+    // barrier): complete them here so no wave reads the stage before they land
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
 
   f32x4 acc[FM][FN];

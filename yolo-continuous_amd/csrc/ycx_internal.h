@@ -110,7 +110,8 @@ __device__ __forceinline__ void ycx_class_finish(F&& logit, float m, float pm, i
   const float sm = ycx_sigmoid(m);
   best = sm;
   bi = b;
-  if (pm == -INFINITY) return;  // nothing before bi can reach sm
+  // nothing before bi can reach sm -- unless sm is 0: then an earlier -inf ties it
+  if (pm == -INFINITY && sm > 0.0f) return;
   float tau = fmaxf(fabsf(m), 1.0f) * 0x1p-12f, lo = m < INFINITY ? m - tau : -INFINITY;
   for (int i = 0; i < 6 && ycx_sigmoid(lo) == sm; ++i) {  // saturated: widen until sigmoid drops
     tau *= 16.0f;

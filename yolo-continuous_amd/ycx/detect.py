@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -268,6 +269,12 @@ class DevicePost:
         return self.dets, self.keep, self.kc
 
 
+def _release_engine(model_ref, shape, device, slot):
+    model = model_ref()
+    if model is not None:
+        model.release_slot(shape, device, slot)
+
+
 class Detector:
     """Fused device pipeline for a fixed batch shape: Model forward (static plan,
     optionally one HIP graph) -> candidates -> ycx_sort_nms (DevicePost).
@@ -288,8 +295,13 @@ class Detector:
         self.model = model
         # a private engine unless the caller names a slot: the static buffers of one
         # Detector must never alias model(x)'s or another Detector's (in flight on
-        # another stream)
-        self.engine = model.engine_for(shape, device, model.new_slot() if slot is None else slot)
+        # another stream). A private engine lives as long as this Detector: close()
+        # (or the finaliser, when the Detector is collected) drops it from the model.
+        own = slot is None
+        slot = model.new_slot() if own else slot
+        self.engine = model.engine_for(shape, device, slot)
+        self._release = (weakref.finalize(self, _release_engine, weakref.ref(model), tuple(shape), str(device), slot)
+                         if own else None)
         self.device = torch.device(device)
         n, _, H, W = shape
         image_size = image_size or (H, W)
@@ -312,6 +324,14 @@ class Detector:
 
     def post(self):
         return self._post()
+
+    def close(self):
+        """Release this Detector's private engine (activations, packed weights,
+        HIP graph). Work already queued on its buffers must have completed; the
+        Detector is unusable afterwards."""
+        if self._release is not None:
+            self._release()
+        self.engine = None
 
     def forward(self, events=None):
         """The model forward on the static input buffer (current stream); with
@@ -381,6 +401,13 @@ class PipelinedDetector:
         cur.wait_stream(self.s_fwd)
         cur.wait_stream(self.s_post)
 
+    def close(self):
+        """Wait for the batches in flight, then release every slot's engine."""
+        self.synchronize()
+        torch.cuda.synchronize(self.device)
+        for d in self.slots:
+            d.close()
+
 
 class ConcurrentDetector:
     """``depth`` batches in flight, each on its own slot and HIP stream: batch i
@@ -439,6 +466,13 @@ class ConcurrentDetector:
         cur = torch.cuda.current_stream(self.device)
         for s in self.streams:
             cur.wait_stream(s)
+
+    def close(self):
+        """Wait for the batches in flight, then release every slot's engine."""
+        self.synchronize()
+        torch.cuda.synchronize(self.device)
+        for d in self.slots:
+            d.close()
 
 
 def prepare_model(plan, weights=None, device=None, precision='bf16'):

@@ -273,6 +273,19 @@ _TILE_MAP = {int(a): [int(t) for t in b.split('/')] for a, b in
              (kv.split(':') for kv in os.environ.get('YCX_TILE_MAP', '').split(',') if kv)}
 
 
+def cascade_fits(h, w, c, esz):
+    """Whether ycx_maxpool's one-launch cascade (levels > 1) takes an (h, w) map of c
+    channels of esz bytes: it keeps two copies of the H x W plane of one channel
+    slice (a 16-byte multiple dividing c, at most 128 channels) in 64 KB of LDS
+    (ycx_misc.hip, ycx_maxpool). Mirrors the launcher's slice search exactly."""
+    t = 128
+    while t * esz >= 16:
+        if c % t == 0 and 2 * h * w * t * esz <= 65536:
+            return True
+        t >>= 1
+    return False
+
+
 class Plan:
     """Device-independent lowering of a Model for one input shape: the graph
     after all passes, its outputs and its algorithmic FLOPs."""
@@ -707,7 +720,9 @@ class Engine:
         """Chains of 'same' stride-1 pools (the SPPCSPC k5 cascade, `pyramid`), each pool
         reading the previous one's output, written to adjacent slices of one buffer: run as
         one ycx_maxpool launch with levels = chain length (bf16 / fp8 plans, HIP_CASCADE
-        kernel). Returns {id(first pool): [pool nodes]}."""
+        kernel), when the map's plane fits the kernel's LDS (``cascade_fits``; larger maps,
+        e.g. the stride-32 map of a 1472^2 input, keep one launch per pool).
+        Returns {id(first pool): [pool nodes]}."""
         if self.dt not in (L.DT_BF16, L.DT_FP8) or os.environ.get('YCX_NO_POOL_CASCADE'):
             return {}
         nodes, out = self.graph.nodes, {}
@@ -719,6 +734,8 @@ class Engine:
 
         for i, a in enumerate(nodes):
             if id(a) in used or not same_pool(a) or a.out.role in ('input', 'output'):
+                continue
+            if not cascade_fits(a.inputs[0].h, a.inputs[0].w, a.inputs[0].c, self.dtype.itemsize):
                 continue
             chain = [a]
             for b in nodes[i + 1:]:

@@ -224,6 +224,15 @@ class Model(nn.Module):
         self._slot_counter = getattr(self, '_slot_counter', 0) + 1
         return 1000 + self._slot_counter
 
+    def release_slot(self, shape, device, slot):
+        """Drop the engine of one slot (its activation buffers, packed weights and
+        HIP graph). Detectors call this from close() / their finaliser."""
+        key = (tuple(int(s) for s in shape), str(torch.device(device)), self.precision, int(slot))
+        eng = getattr(self, '_engines', {}).pop(key, None)
+        if eng is not None:
+            eng.close()
+        return eng is not None
+
     def engine_for(self, shape, device, slot=0):
         """The compiled plan for (shape, device, precision); every distinct
         ``slot`` is an independent copy (own activation buffers). ``forward``
