@@ -234,6 +234,11 @@ const char* ycx_conv_tile_name(int32_t tile);
 /* The tile ycx_conv2d uses for d->tile == 0. d->res_c_stride > 0 means the
  * call will pass a residual (tile 22, the weight-resident 1x1, takes none). */
 int32_t ycx_conv_pick_tile(const ycx_conv_desc* d);
+/* Introspection (host only, no device call): the (output-channel tile, pixel
+ * tile) that workgroup `bid` of an LDS-DMA conv launch of nwg = n_ct * n_pt
+ * workgroups computes under channel-group count gc (the XCD region map), as
+ * ct * 65536 + pt; -1 on bad arguments. Lets tests prove the map bijective. */
+int32_t ycx_conv_tile_of(int32_t bid, int32_t nwg, int32_t n_ct, int32_t gc);
 
 ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const void* w,
                       const float* bias, void* y, const void* residual, void* stream);

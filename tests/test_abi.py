@@ -84,3 +84,23 @@ def test_missing_library_fails_loudly(tmp_path):
     pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "yolo-continuous_amd")
     r = subprocess.run([sys.executable, "-c", "import ycx._lib"], cwd=pkg, env=env, capture_output=True, text=True)
     assert r.returncode != 0 and "no CPU fallback" in r.stderr
+
+
+@pytest.mark.parametrize('gc', [0, 1, 2, 4, 8])
+def test_conv_tile_map_is_a_bijection(gc):
+    """The XCD region map of the LDS-DMA conv tiles (ycx_tile_of) visits every
+    (channel tile, pixel tile) exactly once for any grid, including pixel-tile
+    counts that do not split evenly over the XCD regions (host-side call, no GPU)."""
+    from ycx import _lib as L
+    for n_ct in (1, 2, 3, 4, 8, 16):
+        for n_pt in (1, 3, 7, 25, 100, 101, 800):
+            nwg = n_ct * n_pt
+            seen = set()
+            for b in range(nwg):
+                v = int(L.lib.ycx_conv_tile_of(b, nwg, n_ct, gc))
+                assert v >= 0
+                ct, pt = divmod(v, 65536)
+                assert 0 <= ct < n_ct and 0 <= pt < n_pt
+                seen.add((ct, pt))
+            assert len(seen) == nwg, (gc, n_ct, n_pt)
+    assert L.lib.ycx_conv_tile_of(0, 10, 3, 2) == -1   # nwg not a multiple of n_ct

@@ -25,8 +25,9 @@ pytestmark = pytest.mark.gpu
 A = np.asarray(ANCHORS).reshape(-1, 2)
 C2_BAR, C5_BAR = 1e-2, 0.10   # heads: max |gpu - oracle| / max |oracle| (bf16, fp8 e4m3); measured r02: 0.0045, 0.088
 # end-to-end keep-set differences over the FULL survivor lists (images 0 / n-1), all from
-# sigmoid/exp ulps in the device decode (nms_exact holds); provisional until measured
-KEEP_FLIPS_PIN = {'c2': 60, 'c5': 60, 'c4': 12}
+# sigmoid/exp ulps in the device decode (nms_exact holds on the device's own candidates);
+# measured r03 on MI355X: c2 3 / 0 of 9725 / 9754 kept, c5 0 / 0 of 9685 / 9659, c4 6 of 38781
+KEEP_FLIPS_PIN = {'c2': 6, 'c5': 4, 'c4': 12}
 
 
 @pytest.fixture(scope='module')

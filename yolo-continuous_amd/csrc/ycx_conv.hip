@@ -22,6 +22,7 @@
 // f32 path ("parity mode"): same structure on v_mfma_f32_16x16x4_f32 (exact
 // fp32 FMA chain), used to prove the 1e-3 relative bound vs the fp32 CPU
 // reference.
+#include <stdlib.h>
 #include <algorithm>
 #include <type_traits>
 #include "ycx_internal.h"
@@ -44,6 +45,7 @@ struct ConvArgs {
   int M, HoWo, Ktot, nsteps, n_ct, nwg;
   float out_scale, res_scale;  // YCX_DT_FP8 only
   int pool;                    // x is the (2H, 2W) map of a fused k2 s2 max-pool (ycx_conv_desc.in_pool)
+  int gc;                      // LDS-DMA tiles: channel groups of the XCD region map (ycx_tile_of)
 };
 
 template <int BK>
@@ -660,7 +662,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
 #endif
   const int wm = wid / WN, wn = wid % WN;
   const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
-  const int ct = L % a.n_ct, pt = L / a.n_ct;
+  int ct, pt;
+  ycx_tile_of(L, a.n_ct, a.nwg / a.n_ct, a.gc, ct, pt);
   const int co0 = ct * BM, px0 = pt * BN;
   const int lrow = lane >> 3, pch = lane & 7;  // row within the 8-row wave slab, physical chunk
 
@@ -1127,7 +1130,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a, HeadArg
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
-  const int ct = L % a.n_ct, pt = L / a.n_ct;
+  int ct, pt;
+  ycx_tile_of(L, a.n_ct, a.nwg / a.n_ct, a.gc, ct, pt);
   const int co0 = ct * BM, px0 = pt * BN;
   const int lrow = lane >> 3, pch = lane & 7;
 
@@ -2719,7 +2723,7 @@ ConvArgs make_args(const ycx_conv_desc* d, const void* x, const void* w, const f
   a.res_coff = d->res_c_off; a.res_cs = d->res_c_stride;
   a.M = d->n * d->ho * d->wo; a.HoWo = d->ho * d->wo; a.Ktot = d->kh * d->kw * d->cin;
   if (d->dtype == YCX_DT_FP8) a.Ktot = (a.Ktot + 127) / 128 * 128;  // padded weight row (bytes)
-  a.nsteps = 0; a.n_ct = 0; a.nwg = 0;
+  a.nsteps = 0; a.n_ct = 0; a.nwg = 0; a.gc = 0;
   a.out_scale = d->out_scale; a.res_scale = d->res_scale;
   a.pool = d->in_pool;
   return a;
@@ -2814,6 +2818,17 @@ ycx_status launch_halo(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
+// Channel groups of the XCD region map (ycx_tile_of) for an LDS-DMA tile launch.
+// YCX_GLDS_GC (development A/B) forces one value for every launch.
+int glds_gc(const ConvArgs& a) {
+  static const int forced = [] {
+    const char* e = getenv("YCX_GLDS_GC");
+    return e ? atoi(e) : -1;
+  }();
+  if (forced >= 0) return forced;
+  return 0;
+}
+
 template <int BM, int BN, int WM, int WN, bool TT = false, int NST = 3, int NSB = NST>
 ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   if (TT && a.Cin != 32) return YCX_ERR_UNSUPPORTED;
@@ -2821,6 +2836,7 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   a.nsteps = TT ? (a.KH * a.KW + 1) / 2 : a.KH * a.KW * (a.Cin / 64);
   a.n_ct = a.Cout_pad / BM;
   a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
+  a.gc = glds_gc(a);
   if constexpr (!TT && NST == 2 && NSB == 2 && BN == 128) {  // tiles 16, 18, 25
     if (a.pool) {
       if (a.KH != 1 || a.KW != 1 || a.S != 1 || a.P != 0) return YCX_ERR_UNSUPPORTED;
@@ -2866,6 +2882,7 @@ ycx_status launch_f8(ConvArgs a, hipStream_t st) {
   if (a.nsteps * 128 != a.Ktot) return YCX_ERR_UNSUPPORTED;  // weight rows padded to whole K steps
   a.n_ct = a.Cout_pad / BM;
   a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
+  a.gc = glds_gc(a);
   const dim3 g(a.nwg), b(WM * WN * 64);
   if (tps == 4) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 4>), g, b, 0, st, a, HeadArgs{});
   else if (tps == 2) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 2>), g, b, 0, st, a, HeadArgs{});
@@ -3057,6 +3074,13 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
   if ((M + 255) / 256 >= 512) return 15;  // tests/probes/conv_bench.py: 80^2 x bs 32 128->64 3x3 48.7 vs 52.3 us (t18)
   if ((d->cout_pad / 64) * ((M + 127) / 128) >= 256) return 18;
   return 3;
+}
+
+extern "C" int32_t ycx_conv_tile_of(int32_t bid, int32_t nwg, int32_t n_ct, int32_t gc) {
+  if (nwg <= 0 || n_ct <= 0 || nwg % n_ct || bid < 0 || bid >= nwg || nwg / n_ct >= 65536) return -1;
+  int ct, pt;
+  ycx_tile_of(ycx_xcd_remap(bid, nwg), n_ct, nwg / n_ct, gc, ct, pt);
+  return ct * 65536 + pt;
 }
 
 extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {

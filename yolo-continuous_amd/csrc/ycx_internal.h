@@ -48,9 +48,34 @@ __device__ __forceinline__ float act_t(float v, float slope) {
 // XCD-aware bijective remap of a 1-D block id (guide §5 "XCD swizzle must be
 // bijective"): consecutive logical ids land on the same XCD (blocks b, b+8, ...
 // share one), so blocks that share an activation tile share an L2.
-__device__ __forceinline__ int ycx_xcd_remap(int bid, int nwg) {
+__host__ __device__ __forceinline__ int ycx_xcd_remap(int bid, int nwg) {
   int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// Logical block L (after ycx_xcd_remap: each XCD holds a contiguous range of L)
+// -> (output-channel tile ct, pixel tile pt) of an n_ct x n_pt tile grid.
+// gc <= 1: ct fastest (every XCD walks every ct over its 1/8 of the pixel tiles,
+// i.e. streams the whole weight tensor through its L2). gc in {2, 4, 8} with
+// n_ct % gc == 0: the grid is cut into 8 regions, gc channel groups x 8/gc pixel
+// groups, enumerated region by region (ct fastest inside a region), so the
+// region an XCD's range covers reads 1/gc of the weights and gc/8 of the
+// pixels: weights are re-read 8/gc times instead of 8, activations gc times.
+// Bijective by construction (an ordering of all tiles).
+__host__ __device__ __forceinline__ void ycx_tile_of(int L, int n_ct, int n_pt, int gc, int& ct, int& pt) {
+  if (gc <= 1 || n_ct % gc) {
+    ct = L % n_ct;
+    pt = L / n_ct;
+    return;
+  }
+  const int gp = 8 / gc, nct_r = n_ct / gc;
+  int pg = 0;  // largest pg with n_ct * pt_lo(pg) <= L, pt_lo(pg) = pg * n_pt / gp
+  const int q = L / n_ct;
+  while (pg + 1 < gp && (pg + 1) * n_pt / gp <= q) ++pg;
+  const int lo = pg * n_pt / gp, npt = (pg + 1) * n_pt / gp - lo;
+  const int rem = L - n_ct * lo, cg = rem / (nct_r * npt), r2 = rem - cg * (nct_r * npt);
+  ct = cg * nct_r + r2 % nct_r;
+  pt = lo + r2 / nct_r;
 }
 
 // torch.sigmoid as the decode kernels evaluate it (detect.py:53, 1/(1+e^-v),

@@ -119,6 +119,7 @@ _SIGS = [
     ("ycx_strerror", ctypes.c_char_p, [_i32]),
     ("ycx_conv_tile_name", ctypes.c_char_p, [_i32]),
     ("ycx_conv_pick_tile", _i32, [ctypes.POINTER(ConvDesc)]),
+    ("ycx_conv_tile_of", _i32, [_i32, _i32, _i32, _i32]),
     ("ycx_conv2d", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP]),
     ("ycx_conv2d_head", _i32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(HeadDesc), _VP, _VP, _VP, _VP, _VP, _VP,
                                _VP, _VP]),
