@@ -94,6 +94,9 @@ def parse(argv=None):
     ap.add_argument("--obj-shift", type=float, default=-3.0, help="--post-micro: objectness logit shift")
     ap.add_argument("--diag-forward-only", action="store_true",
                     help="DIAGNOSTIC (not the metric): time the forwards alone, no decode / NMS")
+    ap.add_argument("--image-in-steps", type=int, default=30,
+                    help="image-in leg (SURVEY 8(d) H2D-inclusive variant): seeded 512x773 uint8 BGR host images "
+                         "in pinned memory -> H2D -> ycx_letterbox_batch -> the same path; 0: skip")
     ap.add_argument("--round", default=None,
                     help="profiles/<round>/traffic.json for roofline.traffic (default: the newest round that has one)")
     ap.add_argument("--dry-run", action="store_true",
@@ -346,6 +349,67 @@ def post_micro(args, dev):
     print(json.dumps(out), flush=True)
 
 
+def image_in_leg(args, det, dev, dist_on, gather):
+    """SURVEY 8(d) "H2D-inclusive variant" / 8(f)1: the step starts from host
+    images, as detect.py:16-26 does (cv2 image -> letterbox -> tensor): seeded
+    512x773x3 uint8 BGR images in pinned host memory; on each batch's slot stream
+    one async H2D copy into a device staging buffer, one ycx_letterbox_batch into
+    the slot's input, then the same forward + decode + NMS (+ gather). Returns
+    the loaded rate (batches in flight, copies overlapping other batches'
+    kernels) and the unloaded host-to-detections latency of one batch alone."""
+    from ycx.utils.letterbox import letterbox_batch_gpu
+    n, h0, w0 = args.batch, 512, 773
+    g = torch.Generator().manual_seed(2024)
+    host = torch.randint(0, 256, (n, h0, w0, 3), dtype=torch.uint8, generator=g).pin_memory()
+    slots = det.slots if hasattr(det, 'slots') else [det]
+    stage = [torch.empty((n, h0, w0, 3), dtype=torch.uint8, device=dev) for _ in slots]
+
+    def pre(k, d):
+        stage[k].copy_(host, non_blocking=True)
+        letterbox_batch_gpu(stage[k], d.x)
+
+    def step():
+        if hasattr(det, 'slots'):
+            return det.submit(pre=pre, then=gather if dist_on else None)[2]
+        pre(0, det)
+        return det()[2]
+
+    def drain():
+        if hasattr(det, 'slots'):
+            det.synchronize()
+        torch.cuda.synchronize()
+
+    for _ in range(3):
+        step()
+    drain()
+    if dist_on:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.image_in_steps):
+        step()
+    drain()
+    if dist_on:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    lat = []
+    for _ in range(max(3, min(10, args.image_in_steps))):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        step()
+        drain()
+        lat.append((time.perf_counter() - t1) * 1e3)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist_on:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    world = dist.get_world_size() if dist_on else 1
+    return dict(value_image_in=round(world * n * args.image_in_steps / float(t.item()), 2),
+                ms_per_step_image_in=round(float(t.item()) / args.image_in_steps * 1e3, 4),
+                p50_ms_image_in_unloaded=round(statistics.median(lat), 4),
+                image_in=f"{n} seeded {h0}x{w0}x3 uint8 BGR images per GPU per step in pinned host memory "
+                         f"({host.numel() / 1e6:.1f} MB): async H2D + ycx_letterbox_batch to {args.size}x{args.size} "
+                         f"inside the step; {args.image_in_steps} timed steps")
+
+
 def launch_ranks(args, argv):
     """``--gpus N`` (N > 1) without WORLD_SIZE in the environment: start N rank
     processes of this same script, one per GPU (RANK = LOCAL_RANK = i,
@@ -517,6 +581,7 @@ def main(argv=None):
     value = images / elapsed
     det1 = det.slots[0] if pipeline else det
 
+    img_in = image_in_leg(args, det, dev, dist_on, gather) if args.image_in_steps > 0 else None
     rl = roofline(det1, args.roofline_steps, args.precision) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -552,6 +617,7 @@ def main(argv=None):
                          "forward_kernel_ms": round(rl['forward_kernel_ms'], 4)},
             "cpu_baseline": cpu,
             "rccl_world_size": dist.get_world_size() if dist_on else 1,
+            **(img_in or {}),
             "detections_last_step": int(kc.sum().item()),
         }
         print(json.dumps(out), flush=True)

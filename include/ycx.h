@@ -307,6 +307,11 @@ ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, const int32
                         float* dets, int32_t* keep_rows, int32_t* keep_counts, void* stream);
 
 ycx_status ycx_letterbox(const ycx_letterbox_desc* d, const uint8_t* src, float* dst, void* stream);
+/* n same-sized images in one launch: image i is read at src + i * src_image_stride
+ * bytes and written to dst + i * c * out_h * out_w (one NCHW fp32 batch): the
+ * preprocessing of detect.py:16-26 for a whole batch (bench.py --image-in). */
+ycx_status ycx_letterbox_batch(const ycx_letterbox_desc* d, int32_t n, int64_t src_image_stride,
+                               const uint8_t* src, float* dst, void* stream);
 ycx_status ycx_correct_boxes(const ycx_correct_desc* d, float* dets, const int32_t* counts,
                              const int32_t* image_hw, void* stream);
 

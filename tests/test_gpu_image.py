@@ -36,6 +36,19 @@ def test_letterbox_into_batch_slot(device):
         np.testing.assert_array_equal(b[i], ref_letterbox.letterbox_tensor(im, (320, 320)))
 
 
+def test_letterbox_batch_matches_restatement(device):
+    """ycx_letterbox_batch (one launch for a whole batch, bench.py --image-in) ==
+    the CPU restatement image by image, bit for bit."""
+    from ycx.utils.letterbox import letterbox_batch_gpu
+    g = np.random.default_rng(5)
+    imgs = g.integers(0, 256, size=(5, 512, 773, 3), dtype=np.uint8)
+    out = torch.full((5, 3, 640, 640), -1.0, device=device)
+    letterbox_batch_gpu(torch.from_numpy(imgs).to(device), out)
+    got = out.cpu().numpy()
+    for i in range(5):
+        np.testing.assert_array_equal(got[i], ref_letterbox.letterbox_tensor(imgs[i], (640, 640)))
+
+
 @pytest.mark.parametrize('letterbox_image', [True, False])
 @pytest.mark.parametrize('image_hw', [(512, 773), (1080, 1920), (640, 640), (333, 777)])
 def test_correct_boxes_matches_numpy(device, letterbox_image, image_hw):

@@ -10,11 +10,15 @@
 
 namespace {
 
+// blockIdx.y: image of a batch (src advanced by src_image_stride bytes, dst by one
+// c x out_h x out_w image)
 __global__ void __launch_bounds__(256) letterbox_kernel(ycx_letterbox_desc d, const uint8_t* __restrict__ src,
-                                                        float* __restrict__ dst) {
+                                                        float* __restrict__ dst, long long src_image_stride) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
   const int plane = d.out_h * d.out_w;
   if (idx >= plane) return;
+  src += (size_t)blockIdx.y * src_image_stride;
+  dst += (size_t)blockIdx.y * d.c * plane;
   const int oy = idx / d.out_w, ox = idx - oy * d.out_w;
   const int cy = oy - d.top, cx = ox - d.left;
   const bool inside = (unsigned)cy < (unsigned)d.new_h && (unsigned)cx < (unsigned)d.new_w;
@@ -91,17 +95,23 @@ __global__ void __launch_bounds__(256) correct_boxes_kernel(ycx_correct_desc d, 
 
 }  // namespace
 
-extern "C" ycx_status ycx_letterbox(const ycx_letterbox_desc* d, const uint8_t* src, float* dst, void* stream) {
-  YCX_CHECK_ARG(d && src && dst);
+extern "C" ycx_status ycx_letterbox_batch(const ycx_letterbox_desc* d, int32_t n, int64_t src_image_stride,
+                                          const uint8_t* src, float* dst, void* stream) {
+  YCX_CHECK_ARG(d && src && dst && n > 0 && n <= 65535);
   YCX_CHECK_ARG(d->h0 > 0 && d->w0 > 0 && d->c > 0 && d->c <= 4 && d->src_row_stride >= d->w0 * d->c);
   YCX_CHECK_ARG(d->new_h > 0 && d->new_w > 0 && d->top >= 0 && d->left >= 0);
   YCX_CHECK_ARG(d->top + d->new_h <= d->out_h && d->left + d->new_w <= d->out_w);
   YCX_CHECK_ARG(d->pad >= 0 && d->pad <= 255);
+  YCX_CHECK_ARG(n == 1 || src_image_stride >= (int64_t)d->h0 * d->src_row_stride);
   const long long plane = (long long)d->out_h * d->out_w;
-  YCX_CHECK_SUPPORTED(plane < (1LL << 31));
-  hipLaunchKernelGGL(letterbox_kernel, dim3(ycx_cdiv(plane, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     *d, src, dst);
+  YCX_CHECK_SUPPORTED(plane * d->c < (1LL << 31));
+  hipLaunchKernelGGL(letterbox_kernel, dim3(ycx_cdiv(plane, 256), (unsigned)n), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), *d, src, dst, (long long)src_image_stride);
   return ycx_launch_status();
+}
+
+extern "C" ycx_status ycx_letterbox(const ycx_letterbox_desc* d, const uint8_t* src, float* dst, void* stream) {
+  return ycx_letterbox_batch(d, 1, 0, src, dst, stream);
 }
 
 extern "C" ycx_status ycx_correct_boxes(const ycx_correct_desc* d, float* dets, const int32_t* counts,

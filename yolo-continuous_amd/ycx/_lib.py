@@ -126,6 +126,7 @@ _SIGS = [
     ("ycx_stem_conv", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP]),
     ("ycx_idetect_decode", _i32, [ctypes.POINTER(DecodeDesc), ctypes.c_float, _VP, _VP, _VP, _VP]),
     ("ycx_letterbox", _i32, [ctypes.POINTER(LetterboxDesc), _VP, _VP, _VP]),
+    ("ycx_letterbox_batch", _i32, [ctypes.POINTER(LetterboxDesc), _i32, ctypes.c_int64, _VP, _VP, _VP]),
     ("ycx_correct_boxes", _i32, [ctypes.POINTER(CorrectDesc), _VP, _VP, _VP, _VP]),
     ("ycx_stem_conv2", _i32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP,
                               _VP]),

@@ -372,9 +372,10 @@ class PipelinedDetector:
         self.post_done = [torch.cuda.Event() for _ in self.slots]
         self.i = 0
 
-    def submit(self, images=None, timing=None):
+    def submit(self, images=None, timing=None, pre=None, then=None):
         """``timing`` = (start, end) timing events: recorded when the batch's
-        forward starts and when its detections are complete."""
+        forward starts and when its detections are complete. ``pre`` / ``then``
+        as in ConcurrentDetector.submit (forward stream / post stream)."""
         k = self.i % len(self.slots)
         self.i += 1
         det = self.slots[k]
@@ -386,11 +387,15 @@ class PipelinedDetector:
             if images is not None:
                 det.x.copy_(images)
                 images.record_stream(self.s_fwd)  # the caller may free it before this copy runs
+            if pre is not None:
+                pre(k, det)
             det.forward()
             self.fwd_done[k].record(self.s_fwd)
         with torch.cuda.stream(self.s_post):
             self.s_post.wait_event(self.fwd_done[k])
             dets, keep, kc = det.post()
+            if then is not None:
+                dets, keep, kc = then(dets, keep, kc)
             self.post_done[k].record(self.s_post)
             if timing is not None:
                 timing[1].record(self.s_post)
@@ -438,10 +443,12 @@ class ConcurrentDetector:
     def s_post(self):  # the stream of the most recent batch (where its collective goes)
         return self.streams[(self.i - 1) % len(self.slots)]
 
-    def submit(self, images=None, timing=None, then=None, post=True):
-        """Enqueue one batch on the next slot's stream. ``then(dets, keep, kc)``,
-        if given, runs on that stream right after the NMS (the multi-GPU path
-        issues its all-gather there) and its return value replaces the outputs.
+    def submit(self, images=None, timing=None, then=None, post=True, pre=None):
+        """Enqueue one batch on the next slot's stream. ``pre(slot_index, detector)``,
+        if given, runs on that stream first and fills ``detector.x`` (the image-in
+        path: H2D copy + ycx_letterbox_batch). ``then(dets, keep, kc)``, if given,
+        runs on that stream right after the NMS (the multi-GPU path issues its
+        all-gather there) and its return value replaces the outputs.
         ``post=False`` (diagnostics only) enqueues the forward alone."""
         k = self.i % len(self.slots)
         self.i += 1
@@ -453,6 +460,8 @@ class ConcurrentDetector:
             if images is not None:
                 det.x.copy_(images)
                 images.record_stream(s)  # the caller may free it before this copy runs
+            if pre is not None:
+                pre(k, det)
             det.forward()
             dets, keep, kc = det.post() if post else (det.dets, det.keep, det.kc)
             if then is not None:

@@ -64,3 +64,23 @@ def letterbox_gpu(image, new_shape=(640, 640), device=None, out=None, pad=114):
     L.check(L.lib.ycx_letterbox(ctypes.byref(d), src.data_ptr(), out.data_ptr(), L.stream_handle(dev)),
             "ycx_letterbox")
     return out
+
+
+def letterbox_batch_gpu(images, out, pad=114):
+    """A device batch of same-sized HWC uint8 images [n, h0, w0, c] -> letterboxed
+    fp32 NCHW ``out`` [n, c, H, W] in one ycx_letterbox_batch launch on the
+    current stream (detect.py:16-26 for every image of the batch)."""
+    if images.device.type != 'cuda' or out.device != images.device:
+        raise RuntimeError("ycx: letterbox_batch_gpu needs device tensors on one ROCm device")
+    if images.dtype != torch.uint8 or images.dim() != 4 or not images.is_contiguous():
+        raise ValueError("ycx: letterbox_batch_gpu expects a contiguous [n, h, w, c] uint8 tensor")
+    n, h0, w0, c = images.shape
+    rw, rh, top, left, oh, ow = letterbox_geometry(h0, w0, (out.shape[3], out.shape[2]))
+    if tuple(out.shape) != (n, c, oh, ow) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError(f"ycx: letterbox output must be a contiguous fp32 [{n}, {c}, {oh}, {ow}] tensor")
+    d = L.LetterboxDesc()
+    d.h0, d.w0, d.c, d.src_row_stride = h0, w0, c, w0 * c
+    d.out_h, d.out_w, d.new_h, d.new_w, d.top, d.left, d.pad = oh, ow, rh, rw, top, left, pad
+    L.check(L.lib.ycx_letterbox_batch(ctypes.byref(d), n, h0 * w0 * c, images.data_ptr(), out.data_ptr(),
+                                      L.stream_handle(images.device)), "ycx_letterbox_batch")
+    return out
