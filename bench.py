@@ -35,7 +35,7 @@ import torch.distributed as dist  # noqa: E402
 ANCHORS = [[12, 16, 19, 36, 40, 28], [36, 75, 76, 55, 72, 146], [142, 110, 192, 243, 459, 401]]
 MASK = [[6, 7, 8], [3, 4, 5], [0, 1, 2]]
 METRIC = "images/sec (whole node) + p50 end-to-end latency, 640×640 bs=32, 1/2/4/8 MI355X"
-PEAK = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
+PEAK = {"bf16": 2500.0, "fp16": 2500.0, "f32": 157.3, "fp8": 5000.0}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
 
 
 def _current_round():
@@ -64,7 +64,8 @@ def parse(argv=None):
     ap.add_argument("--size", type=int, default=640)
     ap.add_argument("--net", default="yolov7")
     ap.add_argument("--nc", type=int, default=80)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "f32", "fp8"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "f32", "fp8"],
+                    help="fp16: the north_star-conforming mode (1e-3 on box/confidence tensors) at the bf16 rate")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--mode", default="concurrent", choices=["concurrent", "pipelined", "serial"],
                     help="concurrent: 3 batches in flight on 3 streams (default); pipelined: forward and "

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define YCX_ABI_VERSION 6
+#define YCX_ABI_VERSION 7
 
 typedef int32_t ycx_status;
 enum {
@@ -56,8 +56,12 @@ enum {
 /* YCX_DT_FP8: OCP e4m3fn activations and weights (CDNA4 block-scaled MFMA with
  * unit block scales, fp32 accumulate). Each activation buffer carries one
  * power-of-two scale s (stored byte = e4m3(clamp(v * s, +-448))); weights
- * carry one per output channel (see ycx_conv_desc). */
-enum { YCX_DT_BF16 = 0, YCX_DT_F32 = 1, YCX_DT_FP8 = 2 };
+ * carry one per output channel (see ycx_conv_desc).
+ * YCX_DT_F16: IEEE half activations and weights, fp32 accumulate: the bf16
+ * kernels on the f16 MFMA (same rate, 11-bit significand): the precision mode
+ * that holds north_star's 1e-3 at bf16 speed. Activations must stay below
+ * 65504 in magnitude (fp16 range). */
+enum { YCX_DT_BF16 = 0, YCX_DT_F32 = 1, YCX_DT_FP8 = 2, YCX_DT_F16 = 3 };
 enum { YCX_ACT_NONE = 0, YCX_ACT_SILU = 1, YCX_ACT_LEAKY = 2 };
 enum {
   YCX_OUT_NHWC = 0,       /* activation dtype, [N][Ho][Wo][out_c_stride] at out_c_off         */

@@ -24,7 +24,7 @@ def _ref_conv(x_nchw, w, b, s, p, act, slope=0.1):
 def _run_conv(device, n, h, w, cin, cout, k, s, act, tile, dtype, in_extra=0, out_extra=0, residual=False,
               layout=L.OUT_NHWC, seed=0):
     g = torch.Generator().manual_seed(seed)
-    tdt = torch.bfloat16 if dtype == L.DT_BF16 else torch.float32
+    tdt = {L.DT_BF16: torch.bfloat16, L.DT_F16: torch.float16}.get(dtype, torch.float32)
     p = k // 2
     ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
     x = torch.randn(n, h, w, cin + in_extra, generator=g).to(tdt)           # NHWC, slice at in_extra
@@ -72,7 +72,8 @@ def _run_conv(device, n, h, w, cin, cout, k, s, act, tile, dtype, in_extra=0, ou
 
 TILES_BF16 = [(1, 128, 64), (2, 64, 64), (3, 64, 64), (4, 128, 64), (5, 32, 32), (6, 64, 32), (7, 128, 32),
               (9, 128, 64), (10, 64, 64), (11, 256, 128), (12, 128, 64), (13, 64, 32), (14, 128, 32), (14, 256, 32),
-              (15, 64, 64), (16, 128, 64), (17, 64, 32), (18, 64, 128)]
+              (15, 64, 64), (16, 128, 64), (17, 64, 32), (18, 64, 128), (40, 256, 64), (40, 256, 32),
+              (40, 512, 96)]
 
 
 @pytest.mark.parametrize('tile,cout,cin', TILES_BF16)
@@ -81,6 +82,31 @@ def test_conv_bf16_tiles(device, tile, cout, cin, k, s):
     got, ref = _run_conv(device, 2, 13, 11, cin, cout, k, s, L.ACT_SILU, tile, L.DT_BF16, in_extra=8, out_extra=16)
     # bf16 output rounding (2^-8 relative) on top of exact products of bf16 inputs
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize('tile,cout,cin,k,s', [(16, 128, 64, 3, 1), (16, 256, 128, 1, 1), (18, 64, 128, 3, 2),
+                                               (17, 64, 32, 3, 1), (5, 32, 32, 3, 1), (7, 128, 32, 3, 2),
+                                               (1, 128, 64, 3, 1), (11, 256, 128, 3, 1), (40, 256, 64, 3, 1),
+                                               (40, 512, 128, 1, 1)])
+def test_conv_fp16_tiles(device, tile, cout, cin, k, s):
+    """The same tiles built with IEEE half elements (YCX_DT_F16, v_mfma_f32_16x16x32_f16):
+    fp16 output rounding (2^-11 relative) on top of exact products of fp16 inputs."""
+    got, ref = _run_conv(device, 2, 13, 11, cin, cout, k, s, L.ACT_SILU, tile, L.DT_F16, in_extra=8, out_extra=16)
+    torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize('tile,args', [(19, (2, 16, 16, 64, 64, 3, 1)), (20, (2, 32, 48, 128, 256, 3, 1)),
+                                       (22, (2, 13, 11, 256, 248, 1, 1)), (23, (2, 32, 48, 64, 64, 3, 1)),
+                                       (0, (3, 20, 20, 256, 255, 1, 1))])
+def test_conv_fp16_special_kernels(device, tile, args):
+    """fp16 halo (19, 20), weight-resident 1x1 (22), weight-stationary 3x3 (23) and the
+    fp32 NCHW head store."""
+    n, h, w, cin, cout, k, s = args
+    layout = L.OUT_NCHW_F32 if cout == 255 else L.OUT_NHWC
+    extra = 0 if layout == L.OUT_NCHW_F32 else 16
+    got, ref = _run_conv(device, n, h, w, cin, cout, k, s, L.ACT_SILU if cout != 255 else L.ACT_NONE, tile,
+                         L.DT_F16, in_extra=8, out_extra=extra, layout=layout)
+    torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3)
 
 
 @pytest.mark.parametrize('tile', [27, 31, 33])
@@ -126,6 +152,19 @@ def test_conv3x3_ws64(device, n, hw, cout, act):
     """Weight-stationary 3x3 64->64 kernel (tile 23): image borders as halo zeros,
     several tiles per persistent block (double-buffered halo), sliced channels."""
     got, ref = _run_conv(device, n, hw[0], hw[1], 64, cout, 3, 1, act, 23, L.DT_BF16, in_extra=8, out_extra=16)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+
+
+def test_conv_big_tile_residual_up2_slices(device):
+    """Tile 40 (256 x 256 x 32, four stages): residual add, x2 upsample store, channel
+    slices, a ragged pixel tail over several workgroups (M = 2 * 23 * 19 = 874)."""
+    got, ref = _run_conv(device, 2, 23, 19, 128, 256, 3, 1, L.ACT_LEAKY, 40, L.DT_BF16, residual=True,
+                         in_extra=8)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=2e-2)
+    got, ref = _run_conv(device, 2, 23, 19, 64, 512, 1, 1, L.ACT_SILU, 40, L.DT_BF16, layout=L.OUT_NHWC_UP2,
+                         out_extra=8)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+    got, ref = _run_conv(device, 3, 20, 20, 256, 248, 3, 2, L.ACT_SILU, 40, L.DT_BF16, in_extra=16, out_extra=8)
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
 
 

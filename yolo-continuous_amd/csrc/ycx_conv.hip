@@ -27,6 +27,25 @@
 #include <type_traits>
 #include "ycx_internal.h"
 
+// The 16-bit element type of the MFMA conv kernels. This file is compiled twice:
+// as is (bf16: YCX_DT_BF16, and the fp32 / e4m3 paths) and with -DYCX_ELT_F16
+// (IEEE half: YCX_DT_F16, same kernels on v_mfma_f32_16x16x32_f16, which runs at
+// the bf16 rate with three more mantissa bits). The fp16 build's entry points carry
+// an _f16 suffix and are reached through the bf16 build's dtype dispatch.
+#ifdef YCX_ELT_F16
+typedef _Float16 elt_t;
+#define YCX_MFMA16 __builtin_amdgcn_mfma_f32_16x16x32_f16
+#define YCX_DT_ELT YCX_DT_F16
+#define YCX_SFX(name) name##_f16
+#else
+typedef __bf16 elt_t;
+#define YCX_MFMA16 __builtin_amdgcn_mfma_f32_16x16x32_bf16
+#define YCX_DT_ELT YCX_DT_BF16
+#define YCX_SFX(name) name
+#endif
+typedef __attribute__((ext_vector_type(8))) elt_t eltx8;
+typedef __attribute__((ext_vector_type(4))) elt_t eltx4;
+
 namespace {
 
 struct ConvArgs {
@@ -61,7 +80,7 @@ __device__ __forceinline__ void store8(const ConvArgs& a, int p, int co, float v
   if (a.res) {
     const T* r = reinterpret_cast<const T*>(a.res) + (size_t)p * a.res_cs + a.res_coff + co;
     if constexpr (sizeof(T) == 2) {
-      bf16x8 rv = *reinterpret_cast<const bf16x8*>(r);
+      eltx8 rv = *reinterpret_cast<const eltx8*>(r);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
     } else {
@@ -74,10 +93,10 @@ __device__ __forceinline__ void store8(const ConvArgs& a, int p, int co, float v
   auto put = [&](size_t pix) {
     T* o = base + pix * a.out_cs + a.out_coff + co;
     if constexpr (sizeof(T) == 2) {
-      bf16x8 ov;
+      eltx8 ov;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ov[j] = (__bf16)v[j];
-      *reinterpret_cast<bf16x8*>(o) = ov;
+      for (int j = 0; j < 8; ++j) ov[j] = (elt_t)v[j];
+      *reinterpret_cast<eltx8*>(o) = ov;
     } else {
       *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
       *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
@@ -98,25 +117,25 @@ __device__ __forceinline__ void store8(const ConvArgs& a, int p, int co, float v
 // contiguous bytes per pixel and L2 merges the lines), residual added first.
 __device__ __forceinline__ void store4_bf16(const ConvArgs& a, int p, int co, float v[4]) {
   if (a.res) {
-    const bf16x4 rv = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.res) +
+    const eltx4 rv = *reinterpret_cast<const eltx4*>(reinterpret_cast<const elt_t*>(a.res) +
                                                        (size_t)p * a.res_cs + a.res_coff + co);
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] += (float)rv[j];
   }
-  bf16x4 ov;
+  eltx4 ov;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) ov[j] = (__bf16)v[j];
-  __bf16* base = reinterpret_cast<__bf16*>(a.y) + a.out_coff + co;
+  for (int j = 0; j < 4; ++j) ov[j] = (elt_t)v[j];
+  elt_t* base = reinterpret_cast<elt_t*>(a.y) + a.out_coff + co;
   if (a.out_layout == YCX_OUT_NHWC_UP2) {
     const int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
     const size_t W2 = 2 * (size_t)a.Wo;
     const size_t b0 = ((size_t)n * 2 * a.Ho + 2 * oy) * W2 + 2 * ox;
-    *reinterpret_cast<bf16x4*>(base + b0 * a.out_cs) = ov;
-    *reinterpret_cast<bf16x4*>(base + (b0 + 1) * a.out_cs) = ov;
-    *reinterpret_cast<bf16x4*>(base + (b0 + W2) * a.out_cs) = ov;
-    *reinterpret_cast<bf16x4*>(base + (b0 + W2 + 1) * a.out_cs) = ov;
+    *reinterpret_cast<eltx4*>(base + b0 * a.out_cs) = ov;
+    *reinterpret_cast<eltx4*>(base + (b0 + 1) * a.out_cs) = ov;
+    *reinterpret_cast<eltx4*>(base + (b0 + W2) * a.out_cs) = ov;
+    *reinterpret_cast<eltx4*>(base + (b0 + W2 + 1) * a.out_cs) = ov;
   } else {
-    *reinterpret_cast<bf16x4*>(base + (size_t)p * a.out_cs) = ov;
+    *reinterpret_cast<eltx4*>(base + (size_t)p * a.out_cs) = ov;
   }
 }
 
@@ -138,11 +157,11 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
   constexpr int C_BYTES = BN * CP * 4;
   constexpr int LDS_BYTES = STAGE_BYTES > C_BYTES ? STAGE_BYTES : C_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-  __bf16* As = reinterpret_cast<__bf16*>(smem);  // [2][BM*BK]
-  __bf16* Bs = As + 2 * A_EL;                    // [2][BN*BK]
+  elt_t* As = reinterpret_cast<elt_t*>(smem);  // [2][BM*BK]
+  elt_t* Bs = As + 2 * A_EL;                    // [2][BN*BK]
 
-  const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
-  const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
+  const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
+  const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -168,36 +187,36 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
     b_ok[i] = ok;
   }
 
-  bf16x8 ra[ACH], rb[BCH];
-  const bf16x8 zero8 = {};
+  eltx8 ra[ACH], rb[BCH];
+  const eltx8 zero8 = {};
   auto gload = [&](int s, int ky, int kx, int cblk) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       int row = tid / CPR + i * RPP;
       if (row < BM)
-        ra[i] = *reinterpret_cast<const bf16x8*>(Wt + (size_t)(co0 + row) * a.Ktot + s * BK + ch * 8);
+        ra[i] = *reinterpret_cast<const eltx8*>(Wt + (size_t)(co0 + row) * a.Ktot + s * BK + ch * 8);
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       int iy = b_iy0[i] + ky, ix = b_ix0[i] + kx;
       bool ok = b_ok[i] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-      rb[i] = ok ? *reinterpret_cast<const bf16x8*>(
+      rb[i] = ok ? *reinterpret_cast<const eltx8*>(
                        X + ((size_t)(b_nh[i] + iy) * a.W + ix) * a.in_cs + a.in_coff + cblk + ch * 8)
                  : zero8;
     }
   };
   auto lstore = [&](int buf) {
-    __bf16* A = As + buf * A_EL;
-    __bf16* B = Bs + buf * B_EL;
+    elt_t* A = As + buf * A_EL;
+    elt_t* B = Bs + buf * B_EL;
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       int row = tid / CPR + i * RPP;
-      if (row < BM) *reinterpret_cast<bf16x8*>(A + row * BK + ((ch ^ swz<BK>(row)) << 3)) = ra[i];
+      if (row < BM) *reinterpret_cast<eltx8*>(A + row * BK + ((ch ^ swz<BK>(row)) << 3)) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       int row = tid / CPR + i * RPP;
-      if (row < BN) *reinterpret_cast<bf16x8*>(B + row * BK + ((ch ^ swz<BK>(row)) << 3)) = rb[i];
+      if (row < BN) *reinterpret_cast<eltx8*>(B + row * BK + ((ch ^ swz<BK>(row)) << 3)) = rb[i];
     }
   };
 
@@ -208,27 +227,27 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int buf) {
-    const __bf16* A = As + buf * A_EL;
-    const __bf16* B = Bs + buf * B_EL;
+    const elt_t* A = As + buf * A_EL;
+    const elt_t* B = Bs + buf * B_EL;
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       const int c = kk * 4 + (lane >> 4);
-      bf16x8 af[FM], bfr[FN];
+      eltx8 af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         int row = wm * TM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(A + row * BK + ((c ^ swz<BK>(row)) << 3));
+        af[i] = *reinterpret_cast<const eltx8*>(A + row * BK + ((c ^ swz<BK>(row)) << 3));
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         int row = wn * TN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(B + row * BK + ((c ^ swz<BK>(row)) << 3));
+        bfr[j] = *reinterpret_cast<const eltx8*>(B + row * BK + ((c ^ swz<BK>(row)) << 3));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = YCX_MFMA16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
 
@@ -296,7 +315,7 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
     f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * CP + c8 * 8);
     f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * CP + c8 * 8 + 4);
     float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    store8<__bf16>(a, p, co, v);
+    store8<elt_t>(a, p, co, v);
   }
 }
 
@@ -374,7 +393,7 @@ __device__ __forceinline__ void epilogue_frag8(const ConvArgs& a, const f32x4 (&
         v[r] = ycx_act<true>(acc[2 * k][j][r] + b0[r], a.act, a.slope);
         v[4 + r] = ycx_act<true>(acc[2 * k + 1][j][r] + b1[r], a.act, a.slope);
       }
-      store8<__bf16>(a, pxf[j] + (lane & 15), co, v);
+      store8<elt_t>(a, pxf[j] + (lane & 15), co, v);
     }
   }
 }
@@ -401,7 +420,7 @@ __device__ __forceinline__ void epilogue_regs8(const ConvArgs& a, const f32x4 (&
         v[r] = ycx_act<true>(acc[2 * k][j][r] + b0[r], a.act, a.slope);
         v[4 + r] = ycx_act<true>(acc[2 * k + 1][j][r] + b1[r], a.act, a.slope);
       }
-      store8<__bf16>(a, p, co, v);
+      store8<elt_t>(a, p, co, v);
     }
   }
 }
@@ -653,8 +672,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   static_assert(!POOL || (NST == 2 && !SPLIT && !TT && !HEAD), "pooled operand: two-stage [A | B] ring");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
-  const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
-  const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
+  const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
+  const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 #ifdef YCX_GLDS_STAMP
   unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -748,16 +767,16 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   };
   // POOL: the window's four rows of the next K step in flight in registers (no VALU on
   // them before the MFMAs, which would wait for the loads), pooled into LDS after them
-  bf16x8 pw[POOL ? B_PW : 1][4];
+  eltx8 pw[POOL ? B_PW : 1][4];
   auto loadB = [&]() {
     const int cs = a.in_cs, rs = 2 * a.W * a.in_cs;
 #pragma unroll
     for (int i = 0; i < B_PW; ++i) {
-      const __bf16* src = X + (b_base[i] < 0 ? 0 : b_base[i] + i_cb);
-      pw[i][0] = *reinterpret_cast<const bf16x8*>(src);
-      pw[i][1] = *reinterpret_cast<const bf16x8*>(src + cs);
-      pw[i][2] = *reinterpret_cast<const bf16x8*>(src + rs);
-      pw[i][3] = *reinterpret_cast<const bf16x8*>(src + rs + cs);
+      const elt_t* src = X + (b_base[i] < 0 ? 0 : b_base[i] + i_cb);
+      pw[i][0] = *reinterpret_cast<const eltx8*>(src);
+      pw[i][1] = *reinterpret_cast<const eltx8*>(src + cs);
+      pw[i][2] = *reinterpret_cast<const eltx8*>(src + rs);
+      pw[i][3] = *reinterpret_cast<const eltx8*>(src + rs + cs);
     }
     i_cb += BK;
   };
@@ -765,12 +784,12 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     char* base = b_slot(buf);
 #pragma unroll
     for (int i = 0; i < B_PW; ++i) {
-      bf16x8 v;
+      eltx8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        v[j] = (__bf16)fmaxf(fmaxf((float)pw[i][0][j], (float)pw[i][1][j]), fmaxf((float)pw[i][2][j], (float)pw[i][3][j]));
-      if (b_base[i] < 0) v = bf16x8{};
-      *reinterpret_cast<bf16x8*>(base + (wid + NW * i) * 1024 + lane * 16) = v;
+        v[j] = (elt_t)fmaxf(fmaxf((float)pw[i][0][j], (float)pw[i][1][j]), fmaxf((float)pw[i][2][j], (float)pw[i][3][j]));
+      if (b_base[i] < 0) v = eltx8{};
+      *reinterpret_cast<eltx8*>(base + (wid + NW * i) * 1024 + lane * 16) = v;
     }
     // the next raw s_barrier does not wait for LDS stores by itself (gfx950 back-off
     // barrier): complete them here so no wave reads the stage before they land
@@ -837,24 +856,24 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
       if (t + NST - 1 < nt) issue(t + NST - 1, (t + NST - 1) % NST);
     }
     STAMP(3);
-    const __bf16* A = reinterpret_cast<const __bf16*>(a_slot(t % NST));
-    const __bf16* B = reinterpret_cast<const __bf16*>(b_slot(t % NSB));
+    const elt_t* A = reinterpret_cast<const elt_t*>(a_slot(t % NST));
+    const elt_t* B = reinterpret_cast<const elt_t*>(b_slot(t % NSB));
     // all of the stage's fragments are requested before the first MFMA (left to
     // itself the compiler re-reads fragments between MFMAs to save registers,
     // exposing an LDS latency every two MFMAs)
-    bf16x8 af[BK / 32][FM], bfr[BK / 32][FN];
+    eltx8 af[BK / 32][FM], bfr[BK / 32][FN];
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       const int c = kk * 4 + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int row = wm * TM + i * 16 + (lane & 15);
-        af[kk][i] = *reinterpret_cast<const bf16x8*>(A + row * BK + ((c ^ swz<BK>(row)) << 3));
+        af[kk][i] = *reinterpret_cast<const eltx8*>(A + row * BK + ((c ^ swz<BK>(row)) << 3));
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int row = wn * TN + j * 16 + (lane & 15);
-        bfr[kk][j] = *reinterpret_cast<const bf16x8*>(B + row * BK + ((c ^ swz<BK>(row)) << 3));
+        bfr[kk][j] = *reinterpret_cast<const eltx8*>(B + row * BK + ((c ^ swz<BK>(row)) << 3));
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -868,7 +887,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = YCX_MFMA16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
 #ifndef YCX_GLDS_NO_SETPRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -931,6 +950,110 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   }
   if (tid == 0) atomicAdd(&g_glds_stamp[128], 1ull);
 #endif
+}
+
+// -------------------------------------------------------------------------
+// Tile 40: 256 (cout) x 256 (px) per workgroup, 1024 threads (16 waves as 4 x 4, each
+// 64 x 64 = 4 x 4 fragments), 32-deep K stages, NS = 4 stages in LDS (128 KiB, one
+// workgroup per CU) with three in flight. Why: the 128 x 128 two-per-CU tile (16) is
+// bound by the CU's LDS-DMA intake (32 KiB per 2.1 MFLOP: at the ~55-68 GB/s a CU takes
+// in, MFMA stays ~40 % busy); a 256 x 256 tile needs half the bytes per
+// FLOP (32 KiB per 4.2 MFLOP per stage) and three stages in flight hide the DMA latency
+// that a one-workgroup-per-CU two-stage ring exposed (tiles 24-26). Per stage and wave:
+// one 1 KiB LDS-DMA of A rows and one of B rows (16 rows x 64 B), 8 ds_read_b128, 16
+// MFMAs. Rows are 64 B with chunk swizzle swz<32> (conflict-free for the fragment reads:
+// every 16-lane group of ds_read_b128 covers the 64 banks once); the DMA applies it on
+// the source side. A rows are permuted as in conv_bf16_glds so the epilogue stores 16
+// bytes per lane and pixel (epilogue_regs8: bias, act, residual, x2 upsample).
+// -------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) conv_big(ConvArgs a) {
+  constexpr int BM = 256, BN = 256, BK = 32, NS = 4, TM = 64, TN = 64, FM = 4, FN = 4;
+  constexpr int A_BYTES = BM * BK * 2, STAGE = 2 * A_BYTES;  // A then B, 16 KiB each
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+  const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
+  const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
+  const int ct = L % a.n_ct, pt = L / a.n_ct;
+  const int co0 = ct * BM, px0 = pt * BN;
+  const int row = 16 * wid + (lane >> 2), pch = lane & 3;  // this lane's DMA row (A and B) and LDS chunk
+  const int lch = pch ^ swz<BK>(row);                       // logical chunk it fetches
+  const int w_bytes = a.Cout_pad * a.Ktot * 2, x_bytes = a.N * a.H * a.W * a.in_cs * 2;
+  int a_off;
+  {
+    const int f = (row % TM) >> 4, m = row & 15;
+    const int ch = (row / TM) * TM + 32 * (f >> 1) + 8 * (m >> 2) + 4 * (f & 1) + (m & 3);
+    a_off = ((co0 + ch) * a.Ktot + (lch << 3)) * 2;
+  }
+  int b_iy0, b_ix0, b_base;
+  {
+    const int p = px0 + row;
+    const bool ok = p < a.M;
+    const int pp = ok ? p : 0;
+    const int n = pp / a.HoWo, rem = pp - n * a.HoWo;
+    const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    b_iy0 = ok ? oy * a.S - a.P : -(1 << 20);  // tail rows fail the bounds test: zeros
+    b_ix0 = ox * a.S - a.P;
+    b_base = (((n * a.H + b_iy0) * a.W + b_ix0) * a.in_cs + a.in_coff + (lch << 3)) * 2;
+  }
+  int i_ky = 0, i_kx = 0, i_cb = 0;  // K position of the next stage to issue
+  auto issue = [&](int s, int slot) {
+    char* base = smem + slot * STAGE;
+    buf_lds16(Wt, w_bytes, a_off, s * (BK * 2), base + wid * 1024);
+    const bool ok = (unsigned)(b_iy0 + i_ky) < (unsigned)a.H && (unsigned)(b_ix0 + i_kx) < (unsigned)a.W;
+    const int tap = ((i_ky * a.W + i_kx) * a.in_cs + i_cb) * 2;
+    buf_lds16(X, x_bytes, ok ? b_base + tap : 0x7FFFFFF0, 0, base + A_BYTES + wid * 1024);
+    i_cb += BK;
+    if (i_cb == a.Cin) {
+      i_cb = 0;
+      if (++i_kx == a.KW) { i_kx = 0; ++i_ky; }
+    }
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nt = a.nsteps;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nt) issue(s, s);
+  for (int t = 0; t < nt; ++t) {
+    // two DMAs per stage and wave: stage t is complete once at most the younger stages remain
+    const int younger = min(NS - 2, nt - 1 - t);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);  // the slot of stage t - 1, read by all
+    const char* A = smem + (t % NS) * STAGE;
+    const char* B = A + A_BYTES;
+    eltx8 af[FM], bfr[FN];
+    const int c = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int r = wm * TM + i * 16 + (lane & 15);
+      af[i] = *reinterpret_cast<const eltx8*>(A + r * 64 + ((c ^ swz<BK>(r)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int r = wn * TN + j * 16 + (lane & 15);
+      bfr[j] = *reinterpret_cast<const eltx8*>(B + r * 64 + ((c ^ swz<BK>(r)) << 4));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = YCX_MFMA16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  f32x4 bpre[FM];
+  bias8_prefetch<FM>(a, co0 + wm * TM, lane, bpre);
+  epilogue_regs8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane, bpre);
 }
 
 // -------------------------------------------------------------------------
@@ -1341,8 +1464,8 @@ __global__ void __launch_bounds__(512) conv_bf16_p8(ConvArgs a) {
   static_assert(APW >= 1 && BPW >= 1 && FM >= 1 && FN >= 1, "tile");
   __shared__ __attribute__((aligned(1024))) char smem[2 * KTB];
 
-  const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
-  const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
+  const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
+  const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;  // wr: co wave row = the ping-pong group
   const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
@@ -1407,7 +1530,7 @@ __global__ void __launch_bounds__(512) conv_bf16_p8(ConvArgs a) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[m][n][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 af[2][2][FM], bfr[2][2][FN];  // [quadrant][kk][fragment]
+  eltx8 af[2][2][FM], bfr[2][2][FN];  // [quadrant][kk][fragment]
 
   auto read_a = [&](int h, int buf) {
     const char* base = smem + buf * KTB + h * AHB;
@@ -1416,7 +1539,7 @@ __global__ void __launch_bounds__(512) conv_bf16_p8(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wr * QM + i * 16 + (lane & 15), c = kk * 4 + (lane >> 4);
-        af[h][kk][i] = *reinterpret_cast<const bf16x8*>(base + r * 128 + ((c ^ swz<64>(r)) << 4));
+        af[h][kk][i] = *reinterpret_cast<const eltx8*>(base + r * 128 + ((c ^ swz<64>(r)) << 4));
       }
   };
   auto read_b = [&](int h, int buf) {
@@ -1426,7 +1549,7 @@ __global__ void __launch_bounds__(512) conv_bf16_p8(ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int r = wc * QN + j * 16 + (lane & 15), c = kk * 4 + (lane >> 4);
-        bfr[h][kk][j] = *reinterpret_cast<const bf16x8*>(base + r * 128 + ((c ^ swz<64>(r)) << 4));
+        bfr[h][kk][j] = *reinterpret_cast<const eltx8*>(base + r * 128 + ((c ^ swz<64>(r)) << 4));
       }
   };
   auto mfma_q = [&](int m, int n, auto&& dma) {
@@ -1440,7 +1563,7 @@ __global__ void __launch_bounds__(512) conv_bf16_p8(ConvArgs a) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[m][n][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk][i], bfr[n][kk][j], acc[m][n][i][j], 0, 0, 0);
+          acc[m][n][i][j] = YCX_MFMA16(af[m][kk][i], bfr[n][kk][j], acc[m][n][i][j], 0, 0, 0);
       if (DIM && kk == 0) {
         __builtin_amdgcn_sched_barrier(0);
         dma();
@@ -1563,8 +1686,8 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
   constexpr int FM = 2, FN = 4;
   __shared__ __attribute__((aligned(1024))) char smem[WBYTES + 2 * HBUF];
   char* const wl = smem;
-  const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
-  const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
+  const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
+  const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
   const int lrow = lane >> 3, pch = lane & 7;
@@ -1606,7 +1729,7 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
     bv[i] = co < a.Cout ? *reinterpret_cast<const f32x4*>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const bool exact = a.Cout == 64;  // then every tile stores FN times per wave
-  __bf16* __restrict__ Y = reinterpret_cast<__bf16*>(a.y) + a.out_coff;
+  elt_t* __restrict__ Y = reinterpret_cast<elt_t*>(a.y) + a.out_coff;
 
   for (int tile = tb; tile < te; ++tile) {
     const int b = (tile - tb) & 1;
@@ -1626,22 +1749,22 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int lc = kk * 4 + (lane >> 4);
-        bf16x8 af[FM], bfr[FN];
+        eltx8 af[FM], bfr[FN];
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           const int co = 32 * wm + 16 * i + (lane & 15);
-          af[i] = *reinterpret_cast<const bf16x8*>(wl + (t * 64 + co) * 128 + ((lc ^ swz<64>(co)) << 4));
+          af[i] = *reinterpret_cast<const eltx8*>(wl + (t * 64 + co) * 128 + ((lc ^ swz<64>(co)) << 4));
         }
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int h = (wn * FN + j + ky) * HW + (lane & 15) + kx;
-          bfr[j] = *reinterpret_cast<const bf16x8*>(halo + h * 128 + ((lc ^ (h & 7)) << 4));
+          bfr[j] = *reinterpret_cast<const eltx8*>(halo + h * 128 + ((lc ^ (h & 7)) << 4));
         }
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = YCX_MFMA16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
     // epilogue: act, 16-byte stores from registers (no global loads: they would drain vmcnt)
@@ -1652,12 +1775,12 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int p = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0 + (lane & 15);
-        bf16x8 ov;
+        eltx8 ov;
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) ov[4 * i + q] = (__bf16)act_t<ACT>(acc[i][j][q], a.slope);
-        *reinterpret_cast<bf16x8*>(Y + (size_t)p * a.out_cs + co) = ov;
+          for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)act_t<ACT>(acc[i][j][q], a.slope);
+        *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov;
       }
     }
   }
@@ -1676,8 +1799,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3x3_halo(ConvArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[NSTA * A_BYTES + HPIECES * 1024];
   char* halo = smem + NSTA * A_BYTES;
 
-  const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
-  const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
+  const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
+  const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
@@ -1751,22 +1874,22 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3x3_halo(ConvArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int lc = kk * 4 + (lane >> 4);
-      bf16x8 af[FM], bfr[FN];
+      eltx8 af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int row = wm * TM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(As + row * 128 + ((lc ^ swz<64>(row)) << 4));
+        af[i] = *reinterpret_cast<const eltx8*>(As + row * 128 + ((lc ^ swz<64>(row)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int h = (wn * FN + j + ky) * HW + (lane & 15) + kx;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(halo + h * 128 + ((lc ^ (h & 7)) << 4));
+        bfr[j] = *reinterpret_cast<const eltx8*>(halo + h * 128 + ((lc ^ (h & 7)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = YCX_MFMA16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -1978,7 +2101,7 @@ __global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
   const float* Wt = reinterpret_cast<const float*>(a.w);  // [KT][Cout_pad]
   const float* __restrict__ X = reinterpret_cast<const float*>(a.x);
   const int HW = a.H * a.W;
-  bf16x8 af[CT];
+  eltx8 af[CT];
   int dy[8], dx[8], toff[8];
   bool kv[8];
 #pragma unroll
@@ -1990,7 +2113,7 @@ __global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
     dx[j] = tap - dy[j] * KW;
     toff[j] = dc * HW + dy[j] * a.W + dx[j];
 #pragma unroll
-    for (int t = 0; t < CT; ++t) af[t][j] = (__bf16)(kv[j] ? Wt[kk * a.Cout_pad + stem_ch(t, lx)] : 0.0f);
+    for (int t = 0; t < CT; ++t) af[t][j] = (elt_t)(kv[j] ? Wt[kk * a.Cout_pad + stem_ch(t, lx)] : 0.0f);
   }
   float bias[CT][4];
 #pragma unroll
@@ -2011,17 +2134,17 @@ __global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
     const float* Xn = X + (size_t)(n * a.in_cs + a.in_coff) * HW;
     const int iy0 = oy * a.S - a.P, ixl = (ox0 + lx) * a.S - a.P;
     const int base = iy0 * a.W + ixl;
-    bf16x8 b;
+    eltx8 b;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const bool ok = kv[j] && (unsigned)(iy0 + dy[j]) < (unsigned)a.H && (unsigned)(ixl + dx[j]) < (unsigned)a.W;
-      b[j] = (__bf16)(ok ? Xn[base + toff[j]] : 0.0f);
+      b[j] = (elt_t)(ok ? Xn[base + toff[j]] : 0.0f);
     }
 #pragma unroll
     for (int q = 0; q < CT / 2; ++q) {
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2 * q], b, z, 0, 0, 0);
-      const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2 * q + 1], b, z, 0, 0, 0);
+      const f32x4 c0 = YCX_MFMA16(af[2 * q], b, z, 0, 0, 0);
+      const f32x4 c1 = YCX_MFMA16(af[2 * q + 1], b, z, 0, 0, 0);
       const int ch0 = 32 * q + 8 * kq;
       if (ch0 < a.Cout) {
         float o[8];
@@ -2036,10 +2159,10 @@ __global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
           const uint32_t hi = f8x4_pack(o[4] * sc, o[5] * sc, o[6] * sc, o[7] * sc);
           *reinterpret_cast<uint2*>(Y + (size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) = make_uint2(lo, hi);
         } else {
-          bf16x8 ob;
+          eltx8 ob;
 #pragma unroll
-          for (int r = 0; r < 8; ++r) ob[r] = (__bf16)o[r];
-          *reinterpret_cast<bf16x8*>(Y + ((size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) * 2) = ob;
+          for (int r = 0; r < 8; ++r) ob[r] = (elt_t)o[r];
+          *reinterpret_cast<eltx8*>(Y + ((size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) * 2) = ob;
         }
       }
     }
@@ -2106,13 +2229,13 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
   // 32 wm + 8 (lx >> 2) + 4 i + (lx & 3), k = 32 t + 8 kq ..: C rows 4 kq .. +3 of the two fragments
   // are channels 32 wm + 8 kq .. +7, one 16-byte (e4m3: 8-byte) store per lane and pixel)
   static_assert(FM == 2, "channel pairs");
-  const __bf16* __restrict__ Wc = reinterpret_cast<const __bf16*>(ca.w);  // [Cout_pad][3][3][32]
-  bf16x8 aw[9][FM];
+  const elt_t* __restrict__ Wc = reinterpret_cast<const elt_t*>(ca.w);  // [Cout_pad][3][3][32]
+  eltx8 aw[9][FM];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int i = 0; i < FM; ++i)
-      aw[t][i] = *reinterpret_cast<const bf16x8*>(Wc + (size_t)(32 * wm + 8 * (lx >> 2) + 4 * i + (lx & 3)) * ca.Ktot +
+      aw[t][i] = *reinterpret_cast<const eltx8*>(Wc + (size_t)(32 * wm + 8 * (lx >> 2) + 4 * i + (lx & 3)) * ca.Ktot +
                                                   32 * t + 8 * kq);
   f32x4 bvc[FM];
 #pragma unroll
@@ -2123,7 +2246,7 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
   // stem weights / bias / gather offsets (k = 8 kq + j -> tap k / 3, channel k % 3; k >= 27 gathers
   // what lane kq = 2 gathers, a broadcast, and weighs it 0)
   constexpr int KT = 27, CIN = 3;
-  bf16x8 af[2];
+  eltx8 af[2];
   int toff[8];
   {
     const float* Ws = reinterpret_cast<const float*>(sa.w);  // [KT][Cout_pad]
@@ -2133,7 +2256,7 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
       const int tap = kk / CIN, dc = kk - tap * CIN, dy = tap / 3, dx = tap - dy * 3;
       toff[j] = dc * CPS + dy * RS + dx;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) af[t][j] = (__bf16)(kv ? Ws[kk * sa.Cout_pad + stem_ch(t, lx)] : 0.0f);
+      for (int t = 0; t < 2; ++t) af[t][j] = (elt_t)(kv ? Ws[kk * sa.Cout_pad + stem_ch(t, lx)] : 0.0f);
     }
   }
   f32x4 bias_s[2];
@@ -2184,7 +2307,7 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
     s_dst[u] = ok ? s2_slot(r, c) * 64 + 16 * (kq ^ s2_swz(c >> 1)) : kS2Dump * 64 + 16 * kq;
   }
   fetch(tb, 0);
-  __bf16* __restrict__ Y = reinterpret_cast<__bf16*>(ca.y) + ca.out_coff;
+  elt_t* __restrict__ Y = reinterpret_cast<elt_t*>(ca.y) + ca.out_coff;
   // the previous tile's epilogue issued exactly FM x FN stores per wave after
   // this tile's fetch when every channel is stored (vmcnt counts in issue order)
   const bool exact = ca.Cout == FM * 32;
@@ -2205,25 +2328,25 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
     for (int u = 0; u < GPW; ++u) {
       if (u == GPW - 1 && wv + 4 * u >= NGRP) break;  // uniform: the last group is one wave's
       const float* ip = img + s_img[u];  // tap (0, 0), channel 0
-      bf16x8 bq;
+      eltx8 bq;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) bq[j] = (__bf16)ip[toff[j]];
-      const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bq, bias_s[0], 0, 0, 0);
-      const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bq, bias_s[1], 0, 0, 0);
-      bf16x8 o;
+      for (int j = 0; j < 8; ++j) bq[j] = (elt_t)ip[toff[j]];
+      const f32x4 c0 = YCX_MFMA16(af[0], bq, bias_s[0], 0, 0, 0);
+      const f32x4 c1 = YCX_MFMA16(af[1], bq, bias_s[1], 0, 0, 0);
+      eltx8 o;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        o[q] = (__bf16)act_t<ACT1>(c0[q], sa.slope);
-        o[4 + q] = (__bf16)act_t<ACT1>(c1[q], sa.slope);
+        o[q] = (elt_t)act_t<ACT1>(c0[q], sa.slope);
+        o[4 + q] = (elt_t)act_t<ACT1>(c1[q], sa.slope);
       }
-      *reinterpret_cast<bf16x8*>(smem + s_dst[u]) = o;
+      *reinterpret_cast<eltx8*>(smem + s_dst[u]) = o;
       if (u & 1) __builtin_amdgcn_sched_barrier(0);  // two groups in flight: bounded registers
     }
     // border tiles: stem pixels outside the stem map are the second conv's zero padding
     const bool top = sy0 < 0, bottom = sy0 + kS2R > sa.Ho, left = sx0 < 0, right = sx0 + kS2C > sa.Wo;
     if (top || bottom || left || right) {
       __syncthreads();
-      const bf16x8 z8 = {};
+      const eltx8 z8 = {};
       for (int e = tid; e < (kS2R + kS2C) * 2 * 4; e += 256) {  // (row or column, pixel, 16-B chunk)
         const int ch = e & 3, k = e >> 2;
         int r = -1, c = -1;
@@ -2232,7 +2355,7 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
         else if (k < 2 * kS2C + kS2R) { c = left ? 0 : -1; r = k - 2 * kS2C; }
         else { c = right ? sa.Wo - sx0 : -1; r = k - 2 * kS2C - kS2R; }
         if (r >= 0 && c >= 0 && r < kS2R && c < kS2C)
-          *reinterpret_cast<bf16x8*>(smem + s2_slot(r, c) * 64 + 16 * (ch ^ s2_swz(c >> 1))) = z8;
+          *reinterpret_cast<eltx8*>(smem + s2_slot(r, c) * 64 + 16 * (ch ^ s2_swz(c >> 1))) = z8;
       }
     }
     __syncthreads();  // stem tile complete; patch free
@@ -2250,18 +2373,18 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int ky = t / 3, kx = t - 3 * ky;
-      bf16x8 bfr[FN];
+      eltx8 bfr[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int rr = 2 * wn + (j >> 1), cc = 16 * (j & 1) + lx;
         const int slot = (kx & 1) ? kS2R * kS2Even + (2 * rr + ky) * kS2Odd + cc : (2 * rr + ky) * kS2Even + cc + kx / 2;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(smem + slot * 64 + (kx == 2 ? swb1 : swb0));
+        bfr[j] = *reinterpret_cast<const eltx8*>(smem + slot * 64 + (kx == 2 ? swb1 : swb0));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[t][i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = YCX_MFMA16(aw[t][i], bfr[j], acc[i][j], 0, 0, 0);
     }
     // epilogue: bias (in the accumulators) + act, 8 channels of one pixel per lane
     const int co = 32 * wm + 8 * kq;
@@ -2280,10 +2403,10 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
               make_uint2(f8x4_pack(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc),
                          f8x4_pack(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc));
         } else {
-          bf16x8 ov;
+          eltx8 ov;
 #pragma unroll
-          for (int q = 0; q < 8; ++q) ov[q] = (__bf16)v[q];
-          *reinterpret_cast<bf16x8*>(Y + (size_t)p * ca.out_cs + co) = ov;
+          for (int q = 0; q < 8; ++q) ov[q] = (elt_t)v[q];
+          *reinterpret_cast<eltx8*>(Y + (size_t)p * ca.out_cs + co) = ov;
         }
       }
     }
@@ -2303,7 +2426,7 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
 // im2col kernels pull every weight tile into LDS once per block: for
 // 256 x 256 at 160^2 that doubles the bytes moved into LDS). The ring runs
 // across tile boundaries: a full tile's epilogue issues exactly FM x FN
-// bf16x4 stores per wave and those enter the following counted vmcnt waits
+// eltx4 stores per wave and those enter the following counted vmcnt waits
 // (loads, stores and LDS-DMA retire in issue order on gfx950), so the
 // epilogue never drains the ring.
 // Requires 1x1/s1/p0, Cin = 64 KC, NHWC bf16 output without residual.
@@ -2345,14 +2468,14 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
   // this wave's weights (A fragments: row m = lane & 15 of fragment i is channel
   // cob + 8 (m >> 2) + 4 i + (m & 3), k = 32 kq + 8 (lane >> 4) ..): the C rows 4g .. 4g+3 of
   // fragments 0 and 1 are then channels 8g .. 8g+7, one 16-byte store per lane and pixel
-  const __bf16* __restrict__ Wt = reinterpret_cast<const __bf16*>(a.w);
-  bf16x8 af[2 * KC][FM];
+  const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
+  eltx8 af[2 * KC][FM];
   const int m16 = lane & 15;
 #pragma unroll
   for (int kq = 0; kq < 2 * KC; ++kq)
 #pragma unroll
     for (int i = 0; i < FM; ++i)
-      af[kq][i] = *reinterpret_cast<const bf16x8*>(Wt + (size_t)(cob + 8 * (m16 >> 2) + 4 * i + (m16 & 3)) * a.Ktot +
+      af[kq][i] = *reinterpret_cast<const eltx8*>(Wt + (size_t)(cob + 8 * (m16 >> 2) + 4 * i + (m16 & 3)) * a.Ktot +
                                                    32 * kq + 8 * (lane >> 4));
   f32x4 bv[FM];
 #pragma unroll
@@ -2362,7 +2485,7 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
   }
 
   // LDS-DMA: wave-instruction (wid + NW i) fills rows 8 (wid + NW i) .. +7 of a slab
-  const __bf16* __restrict__ X = reinterpret_cast<const __bf16*>(a.x);
+  const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
   const int x_bytes = a.M * a.in_cs * 2;
   const int lrow = lane >> 3, pch = lane & 7;
   int rrow[A_PW], roff[A_PW];
@@ -2387,7 +2510,7 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
   for (int s = 0; s < NS - 1 && s < nst; ++s) issue(s);
 
   const bool exact = a.Cout == a.Cout_pad;  // then every full tile stores exactly NSTO times per wave
-  __bf16* __restrict__ Y = reinterpret_cast<__bf16*>(a.y) + a.out_coff;
+  elt_t* __restrict__ Y = reinterpret_cast<elt_t*>(a.y) + a.out_coff;
   int t = 0;
   for (int tl = 0; tl < t1 - t0; ++tl) {
     f32x4 acc[FM][FN];
@@ -2414,17 +2537,17 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
       for (int kk = 0; kk < 2 * SUB; ++kk) {
         const int c = (kk & 1) * 4 + (lane >> 4);
         const char* Bs = B + (kk >> 1) * SLAB;
-        bf16x8 bfr[FN];
+        eltx8 bfr[FN];
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int row = wp * TPW + j * 16 + (lane & 15);
-          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * 128 + ((c ^ swz<64>(row)) << 4));
+          bfr[j] = *reinterpret_cast<const eltx8*>(Bs + row * 128 + ((c ^ swz<64>(row)) << 4));
         }
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2 * SUB * ks + kk][i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = YCX_MFMA16(af[2 * SUB * ks + kk][i], bfr[j], acc[i][j], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -2433,13 +2556,13 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
     const int co = cob + 8 * (lane >> 4);  // channels co .. co+7 (cout % 8 == 0: all valid or none)
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      bf16x8 ov;
+      eltx8 ov;
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (__bf16)ycx_act<true>(acc[i][j][q] + bv[i][q], a.act, a.slope);
+        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)ycx_act<true>(acc[i][j][q] + bv[i][q], a.act, a.slope);
       const int p = pb + 16 * j;
-      if (p < a.M && co < a.Cout) *reinterpret_cast<bf16x8*>(Y + (size_t)p * a.out_cs + co) = ov;
+      if (p < a.M && co < a.Cout) *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov;
     }
   }
 }
@@ -2775,6 +2898,7 @@ const TileInfo kTiles[] = {
     {64, 256, 64, "f8_halo3x3_ws_co64"},
     {256, 64, 64, "head_co256_px64_decode"},
     {256, 64, 128, "f8_head_co256_px64_decode"},
+    {256, 256, 32, "big_co256_px256_k32_s4"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -2848,6 +2972,16 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   if (a.pool) return YCX_ERR_UNSUPPORTED;
   hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST, NSB>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a,
                      HeadArgs{});
+  return ycx_launch_status();
+}
+
+// tile 40: conv_big (256 x 256 x 32, four stages, one 1024-thread workgroup per CU)
+ycx_status launch_big(ConvArgs a, hipStream_t st) {
+  if (a.Cin % 32 || a.Cout_pad % 256 || a.out_layout == YCX_OUT_NCHW_F32 || a.pool) return YCX_ERR_UNSUPPORTED;
+  a.nsteps = a.KH * a.KW * (a.Cin / 32);
+  a.n_ct = a.Cout_pad / 256;
+  a.nwg = a.n_ct * ((a.M + 255) / 256);
+  hipLaunchKernelGGL(conv_big, dim3(a.nwg), dim3(1024), 0, st, a);
   return ycx_launch_status();
 }
 
@@ -3001,10 +3135,12 @@ ycx_status launch_wres_f8(ConvArgs a, hipStream_t st) {
 
 }  // namespace
 
+#ifndef YCX_ELT_F16  // dtype-independent entry points: once, in the bf16 build
 extern "C" const char* ycx_conv_tile_name(int32_t tile) {
   if (tile < 0 || tile >= kNumTiles) return "invalid";
   return kTiles[tile].name;
 }
+#endif
 
 // Tile heuristic: pick the largest tile that still gives >= ~2 waves of blocks
 // on 256 CUs, with BK = 32 only where cin is not a multiple of 64.
@@ -3076,6 +3212,7 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
   return 3;
 }
 
+#ifndef YCX_ELT_F16
 extern "C" int32_t ycx_conv_tile_of(int32_t bid, int32_t nwg, int32_t n_ct, int32_t gc) {
   if (nwg <= 0 || n_ct <= 0 || nwg % n_ct || bid < 0 || bid >= nwg || nwg / n_ct >= 65536) return -1;
   int ct, pt;
@@ -3088,8 +3225,28 @@ extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {
   return pick_tile(d, d->res_c_stride == 0);  // res_c_stride > 0: the call will pass a residual
 }
 
-extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const void* w, const float* bias,
-                                 void* y, const void* residual, void* stream) {
+// the fp16 build's entry points (ycx_conv.hip compiled with -DYCX_ELT_F16)
+extern "C" ycx_status ycx_conv2d_f16(const ycx_conv_desc*, const void*, const void*, const float*, void*,
+                                     const void*, void*);
+extern "C" ycx_status ycx_conv2d_head_f16(const ycx_conv_desc*, const ycx_head_desc*, const void*, const void*,
+                                          const float*, float*, ycx_cand*, int32_t*, int32_t*, void*);
+extern "C" ycx_status ycx_stem_conv_f16(const ycx_conv_desc*, const float*, const float*, const float*, void*,
+                                        void*);
+extern "C" ycx_status ycx_stem_conv2_f16(const ycx_conv_desc*, const ycx_conv_desc*, const float*, const float*,
+                                         const float*, const void*, const float*, void*, void*);
+#define YCX_TO_F16(cond, call) \
+  do {                         \
+    if (cond) return call;     \
+  } while (0)
+#else
+#define YCX_TO_F16(cond, call) \
+  do {                         \
+  } while (0)
+#endif
+
+extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x, const void* w, const float* bias,
+                                          void* y, const void* residual, void* stream) {
+  YCX_TO_F16(d && d->dtype == YCX_DT_F16, ycx_conv2d_f16(d, x, w, bias, y, residual, stream));
   YCX_CHECK_ARG(d && x && w && bias && y);
   YCX_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->cin > 0 && d->cout > 0 && d->ho > 0 && d->wo > 0);
   YCX_CHECK_ARG(d->kh > 0 && d->kw > 0 && d->stride > 0 && d->pad >= 0);
@@ -3098,11 +3255,11 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
   YCX_CHECK_ARG(d->wo == (d->w + 2 * d->pad - d->kw) / d->stride + 1);
   YCX_CHECK_ARG(d->out_c_off >= 0);
   YCX_CHECK_ARG(d->out_layout == YCX_OUT_NCHW_F32 || d->out_c_off + d->cout <= d->out_c_stride);
-  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
+  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_ELT || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
   YCX_CHECK_SUPPORTED(d->out_layout >= YCX_OUT_NHWC && d->out_layout <= YCX_OUT_NHWC_UP2);
   YCX_CHECK_SUPPORTED(d->act >= YCX_ACT_NONE && d->act <= YCX_ACT_LEAKY);
   YCX_CHECK_SUPPORTED(!residual || d->out_layout == YCX_OUT_NHWC);
-  const int vec = d->dtype == YCX_DT_BF16 ? 8 : d->dtype == YCX_DT_FP8 ? 16 : 4;  // 16-byte DMA chunks
+  const int vec = d->dtype == YCX_DT_ELT ? 8 : d->dtype == YCX_DT_FP8 ? 16 : 4;  // 16-byte DMA chunks
   YCX_CHECK_SUPPORTED(d->in_c_off % vec == 0 && d->in_c_stride % vec == 0);
   if (d->out_layout != YCX_OUT_NCHW_F32)
     YCX_CHECK_SUPPORTED(d->cout % 8 == 0 && d->out_c_off % 8 == 0 && d->out_c_stride % 8 == 0);
@@ -3112,7 +3269,7 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
   YCX_CHECK_SUPPORTED((long long)d->cout_pad * d->kh * d->kw * d->cin < (1LL << 31));
   if (d->in_pool) {  // fused MP: bf16 pointwise over a (2h, 2w) map
     YCX_CHECK_ARG(d->in_pool == 1);
-    YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0);
+    YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_ELT && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0);
     YCX_CHECK_SUPPORTED((long long)d->n * 4 * d->h * d->w * d->in_c_stride * 2 < (1LL << 31));
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -3169,6 +3326,7 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
     case 24: return launch_glds<256, 256, 2, 4, false, 2>(a, st);
     case 25: return launch_glds<256, 128, 2, 4, false, 2>(a, st);
     case 26: return launch_glds<128, 256, 2, 4, false, 2>(a, st);
+    case 40: return launch_big(a, st);
 #ifdef YCX_EXPERIMENTAL_TILES  // retired experiments (tools/build_variant.sh NAME -DYCX_EXPERIMENTAL_TILES)
     case 27: return launch_p8<256, 256>(a, st);
     case 28: return launch_p8<128, 256>(a, st);
@@ -3182,16 +3340,18 @@ extern "C" ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const vo
   }
 }
 
-extern "C" ycx_status ycx_conv2d_head(const ycx_conv_desc* d, const ycx_head_desc* h, const void* x, const void* w,
-                                      const float* bias, float* heads, ycx_cand* cand, int32_t* cand_rows,
-                                      int32_t* cand_counts, void* stream) {
+extern "C" ycx_status YCX_SFX(ycx_conv2d_head)(const ycx_conv_desc* d, const ycx_head_desc* h, const void* x,
+                                               const void* w, const float* bias, float* heads, ycx_cand* cand,
+                                               int32_t* cand_rows, int32_t* cand_counts, void* stream) {
+  YCX_TO_F16(d && d->dtype == YCX_DT_F16,
+             ycx_conv2d_head_f16(d, h, x, w, bias, heads, cand, cand_rows, cand_counts, stream));
   YCX_CHECK_ARG(d && h && x && w && bias && cand && cand_rows && cand_counts);
   YCX_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->cin > 0 && d->cout > 0 && d->ho == d->h && d->wo == d->w);
   YCX_CHECK_ARG(d->in_c_off >= 0 && d->in_c_off + d->cin <= d->in_c_stride && d->cout_pad >= d->cout);
   YCX_CHECK_ARG(h->na > 0 && h->na <= 8 && h->nc > 0 && h->no == h->nc + 5 && h->na * h->no == d->cout);
   YCX_CHECK_ARG(h->row_off >= 0 && h->row_off + h->na * d->ho * d->wo <= h->rows_total);
   const bool f8 = d->dtype == YCX_DT_FP8;
-  YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_BF16 || f8) && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0);
+  YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_ELT || f8) && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0);
   YCX_CHECK_SUPPORTED(d->act == YCX_ACT_NONE && d->out_layout == YCX_OUT_NCHW_F32 && d->cout_pad == 256);
   YCX_CHECK_SUPPORTED(!d->in_pool);
   YCX_CHECK_SUPPORTED(f8 ? (d->in_c_off % 16 == 0 && d->in_c_stride % 16 == 0)
@@ -3205,8 +3365,9 @@ extern "C" ycx_status ycx_conv2d_head(const ycx_conv_desc* d, const ycx_head_des
   return launch_head(a, hd, reinterpret_cast<hipStream_t>(stream), f8);
 }
 
-extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, const float* w, const float* bias,
-                                    void* y, void* stream) {
+extern "C" ycx_status YCX_SFX(ycx_stem_conv)(const ycx_conv_desc* d, const float* x, const float* w,
+                                             const float* bias, void* y, void* stream) {
+  YCX_TO_F16(d && d->dtype == YCX_DT_F16, ycx_stem_conv_f16(d, x, w, bias, y, stream));
   YCX_CHECK_ARG(d && x && w && bias && y);
   YCX_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->cout > 0 && d->cout_pad >= d->cout);
   YCX_CHECK_ARG(d->ho == (d->h + 2 * d->pad - d->kh) / d->stride + 1);
@@ -3215,12 +3376,12 @@ extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, cons
   YCX_CHECK_SUPPORTED(d->cout % 8 == 0 && d->cout_pad % 8 == 0 && d->out_c_off % 8 == 0 &&
                       d->out_c_stride % 8 == 0 && d->out_c_off + d->cout <= d->out_c_stride);
   YCX_CHECK_SUPPORTED(d->out_layout == YCX_OUT_NHWC || d->out_layout == YCX_OUT_NHWC_UP2);
-  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
+  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_ELT || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
   YCX_CHECK_SUPPORTED((long long)d->n * d->ho * d->wo < (1LL << 31) && !d->in_pool);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ConvArgs a = make_args(d, x, w, bias, y, nullptr);
   a.Ktot = d->kh * d->kw * d->cin;  // fp32 stem weights: no fp8 row padding
-  const bool bf = d->dtype == YCX_DT_BF16, f8 = d->dtype == YCX_DT_FP8;
+  const bool bf = d->dtype == YCX_DT_ELT, f8 = d->dtype == YCX_DT_FP8;
   if ((bf || f8) && d->out_layout == YCX_OUT_NHWC && (d->cout_pad == 32 || d->cout_pad == 64) && d->wo % 16 == 0) {
     const long long groups = (long long)a.M / 16;
     dim3 g((unsigned)std::min<long long>((groups + 3) / 4, 256LL * 16));
@@ -3248,7 +3409,7 @@ extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, cons
 #define YCX_STEM(KH_, KW_, CI_)                                                                  \
   if (d->kh == KH_ && d->kw == KW_ && d->cin == CI_) {                                           \
     if (bf)                                                                                      \
-      hipLaunchKernelGGL((stem_kernel<KH_, KW_, CI_, __bf16>), grid, dim3(256), lds, st, a);     \
+      hipLaunchKernelGGL((stem_kernel<KH_, KW_, CI_, elt_t>), grid, dim3(256), lds, st, a);     \
     else if (f8)                                                                                 \
       hipLaunchKernelGGL((stem_kernel<KH_, KW_, CI_, uint8_t>), grid, dim3(256), lds, st, a);    \
     else                                                                                         \
@@ -3265,9 +3426,11 @@ extern "C" ycx_status ycx_stem_conv(const ycx_conv_desc* d, const float* x, cons
   return YCX_ERR_UNSUPPORTED;
 }
 
-extern "C" ycx_status ycx_stem_conv2(const ycx_conv_desc* sd, const ycx_conv_desc* cd, const float* x,
-                                     const float* w_stem, const float* b_stem, const void* w_conv,
-                                     const float* b_conv, void* y, void* stream) {
+extern "C" ycx_status YCX_SFX(ycx_stem_conv2)(const ycx_conv_desc* sd, const ycx_conv_desc* cd, const float* x,
+                                              const float* w_stem, const float* b_stem, const void* w_conv,
+                                              const float* b_conv, void* y, void* stream) {
+  YCX_TO_F16(cd && cd->dtype == YCX_DT_F16,
+             ycx_stem_conv2_f16(sd, cd, x, w_stem, b_stem, w_conv, b_conv, y, stream));
   YCX_CHECK_ARG(sd && cd && x && w_stem && b_stem && w_conv && b_conv && y);
   YCX_CHECK_ARG(sd->n > 0 && sd->h > 0 && sd->w > 0 && cd->n == sd->n);
   YCX_CHECK_ARG(sd->ho == (sd->h + 2 * sd->pad - sd->kh) / sd->stride + 1);
@@ -3282,7 +3445,7 @@ extern "C" ycx_status ycx_stem_conv2(const ycx_conv_desc* sd, const ycx_conv_des
   YCX_CHECK_SUPPORTED(cd->kh == 3 && cd->kw == 3 && cd->stride == 2 && cd->pad == 1 && cd->cin == 32 &&
                       cd->cout_pad == 64 && cd->cout % 8 == 0 && cd->out_c_off % 8 == 0 && cd->out_c_stride % 8 == 0);
   // FP8: the pair computes in bf16 (the stem map never leaves LDS); the output is e4m3 (cd->out_scale)
-  YCX_CHECK_SUPPORTED(sd->dtype == cd->dtype && (cd->dtype == YCX_DT_BF16 || cd->dtype == YCX_DT_FP8) &&
+  YCX_CHECK_SUPPORTED(sd->dtype == cd->dtype && (cd->dtype == YCX_DT_ELT || cd->dtype == YCX_DT_FP8) &&
                       cd->out_layout == YCX_OUT_NHWC);
   YCX_CHECK_SUPPORTED(sd->act >= YCX_ACT_NONE && sd->act <= YCX_ACT_LEAKY && cd->act >= YCX_ACT_NONE &&
                       cd->act <= YCX_ACT_LEAKY);
@@ -3316,7 +3479,7 @@ extern "C" ycx_status ycx_stem_conv2(const ycx_conv_desc* sd, const ycx_conv_des
   return YCX_ERR_UNSUPPORTED;
 }
 
-#ifdef YCX_GLDS_STAMP
+#if defined(YCX_GLDS_STAMP) && !defined(YCX_ELT_F16)
 extern "C" int ycx_debug_glds_stamps(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_glds_stamp), sizeof(g_glds_stamp)) != hipSuccess) return 1;
   if (reset) {

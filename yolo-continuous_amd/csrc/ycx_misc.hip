@@ -21,6 +21,11 @@ struct Vec<__bf16> {
   static constexpr int N = 8;
 };
 template <>
+struct Vec<_Float16> {
+  typedef __attribute__((ext_vector_type(8))) _Float16 type;
+  static constexpr int N = 8;
+};
+template <>
 struct Vec<float> {
   typedef f32x4 type;
   static constexpr int N = 4;
@@ -214,10 +219,14 @@ __global__ void __launch_bounds__(256) quantize_f8_kernel(const float* __restric
 // Cascade of `levels` k x k 'same' max-pools (stride 1) in one launch: one workgroup per
 // (image, CC-channel slice) holds the whole H x W plane in LDS (raw elements), and each level
 // is a row pass then a column pass (a k x k max with -inf padding is separable); level i goes
-// to channels out_c_off + i*c. E = bytes per element (2 bf16, 1 e4m3); 16-byte chunks.
-template <int E>
+// to channels out_c_off + i*c. E = bytes per element (2 bf16 / fp16 (HALF), 1 e4m3); 16-byte chunks.
+template <int E, bool HALF = false>
 __device__ __forceinline__ void chunk_to_f(uint4 v, float (&f)[16 / E]) {
-  if constexpr (E == 2) {
+  if constexpr (E == 2 && HALF) {
+    const _Float16* b = reinterpret_cast<const _Float16*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (float)b[j];
+  } else if constexpr (E == 2) {
     const __bf16* b = reinterpret_cast<const __bf16*>(&v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = (float)b[j];
@@ -227,10 +236,14 @@ __device__ __forceinline__ void chunk_to_f(uint4 v, float (&f)[16 / E]) {
     f8x8_unpack(make_uint2(v.z, v.w), g + 8);
   }
 }
-template <int E>
+template <int E, bool HALF = false>
 __device__ __forceinline__ uint4 f_to_chunk(const float (&f)[16 / E]) {
   uint4 v;
-  if constexpr (E == 2) {
+  if constexpr (E == 2 && HALF) {
+    _Float16* b = reinterpret_cast<_Float16*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = (_Float16)f[j];  // exact: every value is an input element
+  } else if constexpr (E == 2) {
     __bf16* b = reinterpret_cast<__bf16*>(&v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) b[j] = (__bf16)f[j];  // exact: every value is an input element
@@ -243,7 +256,7 @@ __device__ __forceinline__ uint4 f_to_chunk(const float (&f)[16 / E]) {
   return v;
 }
 
-template <int E>
+template <int E, bool HALF = false>
 __global__ void __launch_bounds__(256) maxpool_cascade_kernel(ycx_pool_desc d, int cc, const uint8_t* __restrict__ x,
                                                               uint8_t* __restrict__ y) {
   extern __shared__ uint4 lds_chunks[];
@@ -267,11 +280,11 @@ __global__ void __launch_bounds__(256) maxpool_cascade_kernel(ycx_pool_desc d, i
 #pragma unroll
       for (int j = 0; j < NE; ++j) m[j] = -INFINITY;
       for (int xi = max(xx - r, 0); xi <= min(xx + r, W - 1); ++xi) {
-        chunk_to_f<E>(S[(yy * W + xi) * nchunk + g], f);
+        chunk_to_f<E, HALF>(S[(yy * W + xi) * nchunk + g], f);
 #pragma unroll
         for (int j = 0; j < NE; ++j) m[j] = fmaxf(m[j], f[j]);
       }
-      T[i] = f_to_chunk<E>(m);
+      T[i] = f_to_chunk<E, HALF>(m);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < items; i += blockDim.x) {  // column pass: the level's output
@@ -280,11 +293,11 @@ __global__ void __launch_bounds__(256) maxpool_cascade_kernel(ycx_pool_desc d, i
 #pragma unroll
       for (int j = 0; j < NE; ++j) m[j] = -INFINITY;
       for (int yi = max(yy - r, 0); yi <= min(yy + r, H - 1); ++yi) {
-        chunk_to_f<E>(T[(yi * W + xx) * nchunk + g], f);
+        chunk_to_f<E, HALF>(T[(yi * W + xx) * nchunk + g], f);
 #pragma unroll
         for (int j = 0; j < NE; ++j) m[j] = fmaxf(m[j], f[j]);
       }
-      const uint4 v = f_to_chunk<E>(m);
+      const uint4 v = f_to_chunk<E, HALF>(m);
       S[i] = v;  // the next level's source (every row pass read of S is behind the barrier above)
       *reinterpret_cast<uint4*>(y + ((px0 + pix) * d.out_c_stride + d.out_c_off + lv * d.c + c0) * E + g * 16) = v;
     }
@@ -307,16 +320,18 @@ extern "C" ycx_status ycx_maxpool(const ycx_pool_desc* d, const void* x, void* y
   YCX_CHECK_ARG(d->wo == (d->w + 2 * d->pad - d->k) / d->stride + 1);
   YCX_CHECK_ARG(d->pad * 2 <= d->k);  // torch: pad <= k/2
   YCX_CHECK_ARG(d->in_c_off + d->c <= d->in_c_stride && d->out_c_off + d->c <= d->out_c_stride);
-  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
+  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8 ||
+                      d->dtype == YCX_DT_F16);
   const int vn = d->dtype == YCX_DT_F32 ? 4 : 8;
   YCX_CHECK_SUPPORTED(d->c % vn == 0 && d->in_c_off % vn == 0 && d->in_c_stride % vn == 0 &&
                       d->out_c_off % vn == 0 && d->out_c_stride % vn == 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bool h16 = d->dtype == YCX_DT_F16;
   if (d->levels > 1) {
     YCX_CHECK_ARG(d->stride == 1 && d->k % 2 == 1 && d->pad == d->k / 2 && d->ho == d->h && d->wo == d->w);
     YCX_CHECK_ARG(d->out_c_off + d->levels * d->c <= d->out_c_stride);
-    YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_FP8);
-    const int esz = d->dtype == YCX_DT_BF16 ? 2 : 1;
+    YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_FP8 || h16);
+    const int esz = d->dtype == YCX_DT_FP8 ? 1 : 2;
     // widest channel slice (16-byte multiple, dividing c) whose two planes fit 64 KB of LDS
     const long long hw = (long long)d->h * d->w;
     int cc = 0;
@@ -325,7 +340,10 @@ extern "C" ycx_status ycx_maxpool(const ycx_pool_desc* d, const void* x, void* y
     YCX_CHECK_SUPPORTED(cc > 0);
     const dim3 g((unsigned)(d->n * (d->c / cc)));
     const size_t lds = (size_t)(2 * hw * cc * esz);
-    if (esz == 2)
+    if (h16)
+      hipLaunchKernelGGL((maxpool_cascade_kernel<2, true>), g, dim3(256), lds, st, *d, cc, (const uint8_t*)x,
+                         (uint8_t*)y);
+    else if (esz == 2)
       hipLaunchKernelGGL(maxpool_cascade_kernel<2>, g, dim3(256), lds, st, *d, cc, (const uint8_t*)x, (uint8_t*)y);
     else
       hipLaunchKernelGGL(maxpool_cascade_kernel<1>, g, dim3(256), lds, st, *d, cc, (const uint8_t*)x, (uint8_t*)y);
@@ -336,7 +354,9 @@ extern "C" ycx_status ycx_maxpool(const ycx_pool_desc* d, const void* x, void* y
   if (d->dtype != YCX_DT_FP8 && rows <= 65535 && total < (1LL << 31) &&
       (long long)d->n * d->h * d->w * d->in_c_stride < (1LL << 31)) {
     const dim3 g((unsigned)((rowlen + 255) / 256), (unsigned)rows);
-    if (d->dtype == YCX_DT_BF16)
+    if (h16)
+      hipLaunchKernelGGL(maxpool_rows_kernel<_Float16>, g, dim3(256), 0, st, *d, (const _Float16*)x, (_Float16*)y);
+    else if (d->dtype == YCX_DT_BF16)
       hipLaunchKernelGGL(maxpool_rows_kernel<__bf16>, g, dim3(256), 0, st, *d, (const __bf16*)x, (__bf16*)y);
     else
       hipLaunchKernelGGL(maxpool_rows_kernel<float>, g, dim3(256), 0, st, *d, (const float*)x, (float*)y);
@@ -345,6 +365,9 @@ extern "C" ycx_status ycx_maxpool(const ycx_pool_desc* d, const void* x, void* y
   if (d->dtype == YCX_DT_FP8)
     hipLaunchKernelGGL(maxpool_f8_kernel, dim3(grid_for(total)), dim3(256), 0, st, *d, (const uint8_t*)x,
                        (uint8_t*)y);
+  else if (h16)
+    hipLaunchKernelGGL(maxpool_kernel<_Float16>, dim3(grid_for(total)), dim3(256), 0, st, *d,
+                       (const _Float16*)x, (_Float16*)y);
   else if (d->dtype == YCX_DT_BF16)
     hipLaunchKernelGGL(maxpool_kernel<__bf16>, dim3(grid_for(total)), dim3(256), 0, st, *d,
                        (const __bf16*)x, (__bf16*)y);
@@ -359,7 +382,8 @@ extern "C" ycx_status ycx_copy_channels(const ycx_copy_desc* d, const void* x, v
   YCX_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->c > 0 && (d->scale == 1 || d->scale == 2));
   YCX_CHECK_ARG(d->in_c_off + d->c <= d->in_c_stride && d->out_c_off + d->c <= d->out_c_stride);
   YCX_CHECK_SUPPORTED(d->out_layout == YCX_OUT_NHWC || d->out_layout == YCX_OUT_NCHW_F32);
-  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
+  YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_BF16 || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8 ||
+                      d->dtype == YCX_DT_F16);
   const int vn = d->dtype == YCX_DT_F32 ? 4 : 8;
   YCX_CHECK_SUPPORTED(d->c % vn == 0 && d->in_c_off % vn == 0 && d->in_c_stride % vn == 0 &&
                       d->out_c_off % vn == 0 && d->out_c_stride % vn == 0);
@@ -368,6 +392,9 @@ extern "C" ycx_status ycx_copy_channels(const ycx_copy_desc* d, const void* x, v
   if (d->dtype == YCX_DT_FP8)
     hipLaunchKernelGGL(copy_f8_kernel, dim3(grid_for(total)), dim3(256), 0, st, *d, (const uint8_t*)x,
                        (uint8_t*)y);
+  else if (d->dtype == YCX_DT_F16)
+    hipLaunchKernelGGL(copy_kernel<_Float16>, dim3(grid_for(total)), dim3(256), 0, st, *d, (const _Float16*)x,
+                       (_Float16*)y);
   else if (d->dtype == YCX_DT_BF16)
     hipLaunchKernelGGL(copy_kernel<__bf16>, dim3(grid_for(total)), dim3(256), 0, st, *d, (const __bf16*)x,
                        (__bf16*)y);

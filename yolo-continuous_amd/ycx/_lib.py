@@ -18,11 +18,11 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see above)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("YCX_LIB", os.path.join(_HERE, "libycx_hip.so"))
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # ---- enums (ycx.h) ----
 YCX_OK, YCX_ERR_BAD_ARG, YCX_ERR_UNSUPPORTED, YCX_ERR_LAUNCH, YCX_ERR_CAPACITY = 0, 1, 2, 3, 4
-DT_BF16, DT_F32, DT_FP8 = 0, 1, 2
+DT_BF16, DT_F32, DT_FP8, DT_F16 = 0, 1, 2, 3
 ACT_NONE, ACT_SILU, ACT_LEAKY = 0, 1, 2
 OUT_NHWC, OUT_NCHW_F32, OUT_NHWC_UP2 = 0, 1, 2
 OP_CONV, OP_STEM, OP_POOL, OP_COPY, OP_STEM2, OP_HEAD = 1, 2, 3, 4, 5, 6

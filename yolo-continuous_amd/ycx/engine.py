@@ -458,8 +458,9 @@ class Engine:
                                "there is no CPU path")
         self.plan = Plan(model, shape)
         self.shape, self.device, self.precision = self.plan.shape, device, precision
-        self.dtype = {'bf16': torch.bfloat16, 'f32': torch.float32, 'fp8': torch.float8_e4m3fn}[precision]
-        self.dt = {'bf16': L.DT_BF16, 'f32': L.DT_F32, 'fp8': L.DT_FP8}[precision]
+        self.dtype = {'bf16': torch.bfloat16, 'f32': torch.float32, 'fp8': torch.float8_e4m3fn,
+                      'fp16': torch.float16}[precision]
+        self.dt = {'bf16': L.DT_BF16, 'f32': L.DT_F32, 'fp8': L.DT_FP8, 'fp16': L.DT_F16}[precision]
         self.fuse_stem2 = fuse_stem2
         self.fuse_pool = fuse_pool  # False: every pool writes its map (fp8 calibration reads them all)
         self.prepacked = prepacked  # {'p<i>': packed tensor} from ycx.prepack (skips folding / packing)
@@ -471,6 +472,11 @@ class Engine:
                 raise ValueError("ycx: an fp8 engine needs calibration amax values (Model.calibrate_fp8)")
             self._assign_fp8_scales(fp8_amax)
         self._build()
+
+    @property
+    def h16(self):
+        """The plan runs the 16-bit MFMA kernels (bf16 or IEEE half elements)."""
+        return self.dt in (L.DT_BF16, L.DT_F16)
 
     def activation_bufs(self):
         """The plan's activation buffers in allocation order (the order of
@@ -534,7 +540,7 @@ class Engine:
         """Stem -> 3x3/s2 conv pairs that run as one ycx_stem_conv2 (the stem
         map stays in LDS): bf16, the stem's output read by that conv only."""
         pairs = {}
-        if self.dt not in (L.DT_BF16, L.DT_FP8) or not self.fuse_stem2:
+        if not (self.h16 or self.dt == L.DT_FP8) or not self.fuse_stem2:
             return pairs
         for nd in self.graph.nodes:
             if nd.kind != 'stem':
@@ -610,7 +616,8 @@ class Engine:
 
     def _conv_parts(self, node, bf16_weights=False, pool=None):
         """Packed weights/bias (kept alive in self.params) and the descriptor of a conv/stem node.
-        bf16_weights: bf16 packing whatever the plan dtype (the fp8 stem2 pair computes in bf16).
+        bf16_weights: 16-bit packing whatever the plan dtype (the fp8 stem2 pair computes in bf16;
+        an fp16 plan's pair in fp16).
         pool: the k2 s2 pool node feeding this 1x1 conv, fused into it (``_pool_convs``)."""
         p, x, out = node.p, node.inputs[0], node.out
         w64, b64 = p['w'], p['b']
@@ -621,7 +628,7 @@ class Engine:
         if stem:  # [kh][kw][cin][cout_pad] fp32
             wshape, wdt = (k, k, cin, cpad), torch.float32
         elif bf16_weights:
-            wshape, wdt = (cpad, k, k, cin), torch.bfloat16
+            wshape, wdt = (cpad, k, k, cin), (torch.float16 if self.dt == L.DT_F16 else torch.bfloat16)
         elif f8:  # e4m3 rows of w * s_w[co], [cout_pad][kh*kw*cin padded to 128 B]
             wshape, wdt = (cpad, -(-k * k * cin // 128) * 128), torch.float8_e4m3fn
         else:     # [cout_pad][kh][kw][cin] in the activation dtype
@@ -641,7 +648,7 @@ class Engine:
             if stem:
                 wt = wp.permute(2, 3, 1, 0).contiguous().to(torch.float32)
             elif bf16_weights:
-                wt = wp.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+                wt = wp.permute(0, 2, 3, 1).contiguous().to(wdt)
             elif f8:
                 wt, sw = pack_fp8_weights(wp)
                 bp = torch.cat([bp, 1.0 / (sw * self._scale(x))])  # dq[co] = 1 / (s_w[co] s_x)
@@ -723,7 +730,7 @@ class Engine:
         kernel), when the map's plane fits the kernel's LDS (``cascade_fits``; larger maps,
         e.g. the stride-32 map of a 1472^2 input, keep one launch per pool).
         Returns {id(first pool): [pool nodes]}."""
-        if self.dt not in (L.DT_BF16, L.DT_FP8) or os.environ.get('YCX_NO_POOL_CASCADE'):
+        if not (self.h16 or self.dt == L.DT_FP8) or os.environ.get('YCX_NO_POOL_CASCADE'):
             return {}
         nodes, out = self.graph.nodes, {}
         used = set()
@@ -755,7 +762,7 @@ class Engine:
         conv: the conv pools its operand while staging it (ycx_conv_desc.in_pool, bf16
         plans), so the pooled map is never written. yolov7: all five MP pools.
         Returns {id(conv node): pool node}."""
-        if self.dt != L.DT_BF16 or not self.fuse_pool or os.environ.get('YCX_NO_POOL_FUSE'):
+        if not self.h16 or not self.fuse_pool or os.environ.get('YCX_NO_POOL_FUSE'):
             return {}
         out = {}
         for nd in self.graph.nodes:
@@ -827,7 +834,7 @@ class Engine:
     def head_ops(self):
         """Op index of each output's producing conv, when every output is a bf16 or
         e4m3 Detect-head 1x1 conv the fused kernels cover (ycx_conv2d_head), else None."""
-        if self.dt not in (L.DT_BF16, L.DT_FP8):
+        if not (self.h16 or self.dt == L.DT_FP8):
             return None
         f8 = self.dt == L.DT_FP8
         idx = []

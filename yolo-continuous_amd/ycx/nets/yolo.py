@@ -133,7 +133,7 @@ class WeightInitial(Enum):
     Random = 1
 
 
-PRECISIONS = ('bf16', 'f32', 'fp8')
+PRECISIONS = ('bf16', 'f32', 'fp8', 'fp16')
 
 
 class Model(nn.Module):
@@ -142,8 +142,11 @@ class Model(nn.Module):
     forward(x: fp32 [N, C, H, W] on a ROCm device) -> the last layer's output:
     ``[P5, P4, P3]`` fp32 NCHW logits for a Detect head (nets/detect.py:38).
     ``precision`` selects the kernel dtype: 'bf16' (default, MFMA bf16, fp32
-    accumulate), 'f32' (parity mode, exact-fp32 MFMA) or 'fp8' (OCP e4m3
-    weights and activations on the block-scaled MFMA, fp32 accumulate; the
+    accumulate), 'fp16' (IEEE half activations and weights on the f16 MFMA:
+    the bf16 kernels at the bf16 rate with an 11-bit significand, the mode that
+    holds north_star's 1e-3 on box / confidence tensors; activations must stay
+    inside the fp16 range, |a| < 65504), 'f32' (exact-fp32 MFMA) or 'fp8' (OCP
+    e4m3 weights and activations on the block-scaled MFMA, fp32 accumulate; the
     activation scales come from ``calibrate_fp8``).
     """
 
