@@ -324,6 +324,16 @@ ycx_status ycx_correct_boxes(const ycx_correct_desc* d, float* dets, const int32
  * after the last (per-op kernel timing for the roofline report). */
 ycx_status ycx_run_ops(const ycx_op* ops, int32_t n_ops, void* stream, void* const* events);
 
+/* 1: ycx_run_ops wraps every op in a roctx range "op<i> <kind> <tile> n HxW cin->cout k s"
+ * (rocprofv3 --marker-trace); 0 (default): no tracing. No reference counterpart
+ * (its only instrument is the @timer decorator, utils/helper_torch.py:10-20). */
+void ycx_set_trace(int32_t on);
+/* Kernel-side bounds checks (`make -C yolo-continuous_amd/csrc debug` builds
+ * libycx_hip_dbg.so with -DYCX_DEBUG_BOUNDS; select it with YCX_LIB=<path>): every
+ * conv epilogue store is tested against the output extent its descriptor implies and
+ * skipped if outside. out[0] = violations since the last reset, out[1] = the first
+ * offending source line. YCX_ERR_UNSUPPORTED from a release build. */
+ycx_status ycx_debug_bounds(uint32_t* out, int32_t reset);
 /* Capture ycx_run_ops into a HIP graph and instantiate it (graph_exec out). */
 ycx_status ycx_graph_capture(const ycx_op* ops, int32_t n_ops, void* stream, void** graph_exec);
 ycx_status ycx_graph_launch(void* graph_exec, void* stream);

@@ -23,7 +23,7 @@ from ycx.utils.synth import synthetic_images
 
 pytestmark = pytest.mark.gpu
 
-F32_TOL, BF16_TOL = 2e-3, 2.5e-2   # bf16 measured r02: <= 0.0125 (G2 tiny_640), yolov7 heads ~0.005
+F32_TOL, BF16_TOL = 1e-3, 2.5e-2   # bf16 measured r02: <= 0.0125 (G2 tiny_640), yolov7 heads ~0.005
 F16_TOL = 2e-3
 G1_NAMES = ['conv_k3s1_cin32', 'conv_k3s2_cin32', 'conv_k1_cin64', 'conv_leaky', 'stem_s2_leaky', 'pools',
             'upsample_concat', 'upsample_shared', 'sppcspc', 'repconv', 'csp_blocks', 'detect', 'idetect',

@@ -65,7 +65,11 @@ struct ConvArgs {
   float out_scale, res_scale;  // YCX_DT_FP8 only
   int pool;                    // x is the (2H, 2W) map of a fused k2 s2 max-pool (ycx_conv_desc.in_pool)
   int gc;                      // LDS-DMA tiles: channel groups of the XCD region map (ycx_tile_of)
+  long long out_bytes;         // extent of y the descriptor implies (YCX_DEBUG_BOUNDS store checks)
 };
+// a store of nb bytes at ptr inside the output extent of args A (always true in release builds)
+#define YCX_OUT_OK(A, ptr, nb) \
+  YCX_BOUNDS_OK(reinterpret_cast<const char*>(ptr) - reinterpret_cast<const char*>((A).y), (nb), (A).out_bytes)
 
 template <int BK>
 __device__ __forceinline__ int swz(int row) {
@@ -96,10 +100,10 @@ __device__ __forceinline__ void store8(const ConvArgs& a, int p, int co, float v
       eltx8 ov;
 #pragma unroll
       for (int j = 0; j < 8; ++j) ov[j] = (elt_t)v[j];
-      *reinterpret_cast<eltx8*>(o) = ov;
+      if (YCX_OUT_OK(a, o, sizeof(eltx8))) *reinterpret_cast<eltx8*>(o) = ov;
     } else {
-      *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
-      *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      if (YCX_OUT_OK(a, o, sizeof(f32x4))) *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+      if (YCX_OUT_OK(a, o + 4, sizeof(f32x4))) *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
     }
   };
   if (a.out_layout == YCX_OUT_NHWC_UP2) {
@@ -130,12 +134,12 @@ __device__ __forceinline__ void store4_bf16(const ConvArgs& a, int p, int co, fl
     const int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
     const size_t W2 = 2 * (size_t)a.Wo;
     const size_t b0 = ((size_t)n * 2 * a.Ho + 2 * oy) * W2 + 2 * ox;
-    *reinterpret_cast<eltx4*>(base + b0 * a.out_cs) = ov;
-    *reinterpret_cast<eltx4*>(base + (b0 + 1) * a.out_cs) = ov;
-    *reinterpret_cast<eltx4*>(base + (b0 + W2) * a.out_cs) = ov;
-    *reinterpret_cast<eltx4*>(base + (b0 + W2 + 1) * a.out_cs) = ov;
+    if (YCX_OUT_OK(a, base + b0 * a.out_cs, sizeof(eltx4))) *reinterpret_cast<eltx4*>(base + b0 * a.out_cs) = ov;
+    if (YCX_OUT_OK(a, base + (b0 + 1) * a.out_cs, sizeof(eltx4))) *reinterpret_cast<eltx4*>(base + (b0 + 1) * a.out_cs) = ov;
+    if (YCX_OUT_OK(a, base + (b0 + W2) * a.out_cs, sizeof(eltx4))) *reinterpret_cast<eltx4*>(base + (b0 + W2) * a.out_cs) = ov;
+    if (YCX_OUT_OK(a, base + (b0 + W2 + 1) * a.out_cs, sizeof(eltx4))) *reinterpret_cast<eltx4*>(base + (b0 + W2 + 1) * a.out_cs) = ov;
   } else {
-    *reinterpret_cast<eltx4*>(base + (size_t)p * a.out_cs) = ov;
+    if (YCX_OUT_OK(a, base + (size_t)p * a.out_cs, sizeof(eltx4))) *reinterpret_cast<eltx4*>(base + (size_t)p * a.out_cs) = ov;
   }
 }
 
@@ -286,7 +290,7 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
           int co = co0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
           if (co < a.Cout) {
             float v = ycx_act<true>(acc[i][j][r] + a.bias[co], a.act, a.slope);
-            Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] = v;
+            if (YCX_OUT_OK(a, &Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem], sizeof(Y[0]))) Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] = v;
           }
         }
       }
@@ -341,7 +345,7 @@ __device__ __forceinline__ void epilogue_regs(const ConvArgs& a, const f32x4 (&a
         for (int r = 0; r < 4; ++r) {
           int co = cob + i * 16 + (lane >> 4) * 4 + r;
           if (co < a.Cout)
-            Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] =
+            if (YCX_OUT_OK(a, &Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem], sizeof(Y[0]))) Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] =
                 ycx_act<true>(acc[i][j][r] + bb[i][r], a.act, a.slope);
         }
       }
@@ -1111,12 +1115,12 @@ __device__ __forceinline__ void store4_f8(const ConvArgs& a, int p, int co, floa
     const int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
     const size_t W2 = 2 * (size_t)a.Wo;
     const size_t b0 = ((size_t)n * 2 * a.Ho + 2 * oy) * W2 + 2 * ox;
-    *reinterpret_cast<uint32_t*>(base + b0 * a.out_cs) = o;
-    *reinterpret_cast<uint32_t*>(base + (b0 + 1) * a.out_cs) = o;
-    *reinterpret_cast<uint32_t*>(base + (b0 + W2) * a.out_cs) = o;
-    *reinterpret_cast<uint32_t*>(base + (b0 + W2 + 1) * a.out_cs) = o;
+    if (YCX_OUT_OK(a, base + b0 * a.out_cs, sizeof(uint32_t))) *reinterpret_cast<uint32_t*>(base + b0 * a.out_cs) = o;
+    if (YCX_OUT_OK(a, base + (b0 + 1) * a.out_cs, sizeof(uint32_t))) *reinterpret_cast<uint32_t*>(base + (b0 + 1) * a.out_cs) = o;
+    if (YCX_OUT_OK(a, base + (b0 + W2) * a.out_cs, sizeof(uint32_t))) *reinterpret_cast<uint32_t*>(base + (b0 + W2) * a.out_cs) = o;
+    if (YCX_OUT_OK(a, base + (b0 + W2 + 1) * a.out_cs, sizeof(uint32_t))) *reinterpret_cast<uint32_t*>(base + (b0 + W2 + 1) * a.out_cs) = o;
   } else {
-    *reinterpret_cast<uint32_t*>(base + (size_t)p * a.out_cs) = o;
+    if (YCX_OUT_OK(a, base + (size_t)p * a.out_cs, sizeof(uint32_t))) *reinterpret_cast<uint32_t*>(base + (size_t)p * a.out_cs) = o;
   }
 }
 
@@ -1142,12 +1146,12 @@ __device__ __forceinline__ void store8_f8(const ConvArgs& a, int p, int co, floa
     const int n = p / a.HoWo, rem = p - n * a.HoWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
     const size_t W2 = 2 * (size_t)a.Wo;
     const size_t b0 = ((size_t)n * 2 * a.Ho + 2 * oy) * W2 + 2 * ox;
-    *reinterpret_cast<uint2*>(base + b0 * a.out_cs) = o;
-    *reinterpret_cast<uint2*>(base + (b0 + 1) * a.out_cs) = o;
-    *reinterpret_cast<uint2*>(base + (b0 + W2) * a.out_cs) = o;
-    *reinterpret_cast<uint2*>(base + (b0 + W2 + 1) * a.out_cs) = o;
+    if (YCX_OUT_OK(a, base + b0 * a.out_cs, sizeof(uint2))) *reinterpret_cast<uint2*>(base + b0 * a.out_cs) = o;
+    if (YCX_OUT_OK(a, base + (b0 + 1) * a.out_cs, sizeof(uint2))) *reinterpret_cast<uint2*>(base + (b0 + 1) * a.out_cs) = o;
+    if (YCX_OUT_OK(a, base + (b0 + W2) * a.out_cs, sizeof(uint2))) *reinterpret_cast<uint2*>(base + (b0 + W2) * a.out_cs) = o;
+    if (YCX_OUT_OK(a, base + (b0 + W2 + 1) * a.out_cs, sizeof(uint2))) *reinterpret_cast<uint2*>(base + (b0 + W2 + 1) * a.out_cs) = o;
   } else {
-    *reinterpret_cast<uint2*>(base + (size_t)p * a.out_cs) = o;
+    if (YCX_OUT_OK(a, base + (size_t)p * a.out_cs, sizeof(uint2))) *reinterpret_cast<uint2*>(base + (size_t)p * a.out_cs) = o;
   }
 }
 
@@ -1210,7 +1214,7 @@ __device__ __forceinline__ void epilogue_f8(const ConvArgs& a, const f32x4 (&acc
         for (int r = 0; r < 4; ++r) {
           const int co = cob + i * 16 + (lane >> 4) * 4 + r;
           if (co < a.Cout)
-            Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] =
+            if (YCX_OUT_OK(a, &Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem], sizeof(Y[0]))) Y[((size_t)n * a.out_cs + a.out_coff + co) * a.HoWo + rem] =
                 ycx_act<true>(fmaf(acc[i][j][r], qq[i][r], bb[i][r]), a.act, a.slope);
         }
       }
@@ -1780,7 +1784,7 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)act_t<ACT>(acc[i][j][q], a.slope);
-        *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov;
+        if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov;
       }
     }
   }
@@ -1997,7 +2001,7 @@ __global__ void __launch_bounds__(256) conv_f32_kernel(ConvArgs a) {
         int n2 = pe / a.HoWo, rem2 = pe - n2 * a.HoWo;
         float* Y = reinterpret_cast<float*>(a.y);
         for (int r = 0; r < 4; ++r)
-          if (cb + r < a.Cout) Y[((size_t)n2 * a.out_cs + a.out_coff + cb + r) * a.HoWo + rem2] = v[r];
+          if (cb + r < a.Cout) if (YCX_OUT_OK(a, &Y[((size_t)n2 * a.out_cs + a.out_coff + cb + r) * a.HoWo + rem2], sizeof(Y[0]))) Y[((size_t)n2 * a.out_cs + a.out_coff + cb + r) * a.HoWo + rem2] = v[r];
         continue;
       }
       if (cb >= a.Cout) continue;
@@ -2013,9 +2017,9 @@ __global__ void __launch_bounds__(256) conv_f32_kernel(ConvArgs a) {
         size_t W2 = 2 * (size_t)a.Wo;
         size_t b0 = ((size_t)n2 * 2 * a.Ho + 2 * oy2) * W2 + 2 * ox2;
         size_t q[4] = {b0, b0 + 1, b0 + W2, b0 + W2 + 1};
-        for (int t = 0; t < 4; ++t) *reinterpret_cast<f32x4*>(Y + q[t] * a.out_cs + a.out_coff + cb) = ov;
+        for (int t = 0; t < 4; ++t) if (YCX_OUT_OK(a, Y + q[t] * a.out_cs + a.out_coff + cb, sizeof(f32x4))) *reinterpret_cast<f32x4*>(Y + q[t] * a.out_cs + a.out_coff + cb) = ov;
       } else {
-        *reinterpret_cast<f32x4*>(Y + (size_t)pe * a.out_cs + a.out_coff + cb) = ov;
+        if (YCX_OUT_OK(a, Y + (size_t)pe * a.out_cs + a.out_coff + cb, sizeof(f32x4))) *reinterpret_cast<f32x4*>(Y + (size_t)pe * a.out_cs + a.out_coff + cb) = ov;
       }
     }
 }
@@ -2157,12 +2161,12 @@ __global__ void __launch_bounds__(256) stem_mfma(ConvArgs a) {
           const float sc = a.out_scale;
           const uint32_t lo = f8x4_pack(o[0] * sc, o[1] * sc, o[2] * sc, o[3] * sc);
           const uint32_t hi = f8x4_pack(o[4] * sc, o[5] * sc, o[6] * sc, o[7] * sc);
-          *reinterpret_cast<uint2*>(Y + (size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) = make_uint2(lo, hi);
+          if (YCX_OUT_OK(a, Y + (size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0, sizeof(uint2))) *reinterpret_cast<uint2*>(Y + (size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) = make_uint2(lo, hi);
         } else {
           eltx8 ob;
 #pragma unroll
           for (int r = 0; r < 8; ++r) ob[r] = (elt_t)o[r];
-          *reinterpret_cast<eltx8*>(Y + ((size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) * 2) = ob;
+          if (YCX_OUT_OK(a, Y + ((size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) * 2, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y + ((size_t)(p0 + lx) * a.out_cs + a.out_coff + ch0) * 2) = ob;
         }
       }
     }
@@ -2399,14 +2403,14 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
           for (int q = 0; q < 4; ++q) v[4 * i + q] = act_t<ACT2>(acc[i][j][q], ca.slope);
         if constexpr (F8) {  // the stem map and this conv run in bf16; only the output is e4m3
           const float sc = ca.out_scale;
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(ca.y) + ca.out_coff + (size_t)p * ca.out_cs + co) =
+          if (YCX_OUT_OK(ca, reinterpret_cast<uint8_t*>(ca.y) + ca.out_coff + (size_t)p * ca.out_cs + co, sizeof(uint2))) *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(ca.y) + ca.out_coff + (size_t)p * ca.out_cs + co) =
               make_uint2(f8x4_pack(v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc),
                          f8x4_pack(v[4] * sc, v[5] * sc, v[6] * sc, v[7] * sc));
         } else {
           eltx8 ov;
 #pragma unroll
           for (int q = 0; q < 8; ++q) ov[q] = (elt_t)v[q];
-          *reinterpret_cast<eltx8*>(Y + (size_t)p * ca.out_cs + co) = ov;
+          if (YCX_OUT_OK(ca, Y + (size_t)p * ca.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y + (size_t)p * ca.out_cs + co) = ov;
         }
       }
     }
@@ -2562,7 +2566,7 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)ycx_act<true>(acc[i][j][q] + bv[i][q], a.act, a.slope);
       const int p = pb + 16 * j;
-      if (p < a.M && co < a.Cout) *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov;
+      if (p < a.M && co < a.Cout) if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov;
     }
   }
 }
@@ -2697,7 +2701,7 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
           v[4 * i + q] = ycx_act<true>(fmaf(acc[i][j][q], qv[i][q], bv[i][q]), a.act, a.slope) * osc;
       const uint2 ov = make_uint2(f8x4_pack(v[0], v[1], v[2], v[3]), f8x4_pack(v[4], v[5], v[6], v[7]));
       const int p = pb + 16 * j;
-      if (p < a.M && co < a.Cout) *reinterpret_cast<uint2*>(Y + (size_t)p * a.out_cs + co) = ov;
+      if (p < a.M && co < a.Cout) if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(uint2))) *reinterpret_cast<uint2*>(Y + (size_t)p * a.out_cs + co) = ov;
     }
   }
 }
@@ -2828,7 +2832,7 @@ __global__ void __launch_bounds__(512) conv3x3_ws64_f8(ConvArgs a) {
         float v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = act_t<ACT>(fmaf(acc[i][j][q], qv[i][q], bv[i][q]), a.slope) * osc;
-        *reinterpret_cast<uint32_t*>(Y + (size_t)p * a.out_cs + co) = f8x4_pack(v[0], v[1], v[2], v[3]);
+        if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(uint32_t))) *reinterpret_cast<uint32_t*>(Y + (size_t)p * a.out_cs + co) = f8x4_pack(v[0], v[1], v[2], v[3]);
       }
     }
   }
@@ -2849,6 +2853,11 @@ ConvArgs make_args(const ycx_conv_desc* d, const void* x, const void* w, const f
   a.nsteps = 0; a.n_ct = 0; a.nwg = 0; a.gc = 0;
   a.out_scale = d->out_scale; a.res_scale = d->res_scale;
   a.pool = d->in_pool;
+  {
+    const long long es = d->dtype == YCX_DT_F32 ? 4 : d->dtype == YCX_DT_FP8 ? 1 : 2;
+    const long long px = (long long)d->n * d->ho * d->wo * (d->out_layout == YCX_OUT_NHWC_UP2 ? 4 : 1);
+    a.out_bytes = px * d->out_c_stride * (d->out_layout == YCX_OUT_NCHW_F32 ? 4 : es);
+  }
   return a;
 }
 
@@ -3488,4 +3497,8 @@ extern "C" int ycx_debug_glds_stamps(unsigned long long* out, int reset) {
   }
   return 0;
 }
+#endif
+
+#ifdef YCX_DEBUG_BOUNDS
+extern "C" YCX_DEFINE_BOUNDS_READER(YCX_SFX(ycx_dbg_bounds_conv))
 #endif

@@ -24,6 +24,38 @@ static inline ycx_status ycx_launch_status() {
 
 static inline unsigned ycx_cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
 
+// Kernel-side bounds checks (`make debug` -> libycx_hip_dbg.so, built with
+// -DYCX_DEBUG_BOUNDS): every guarded global store first tests its element range
+// against the buffer extent the descriptor implies; a store outside it is skipped and
+// counted (first offending source line kept) instead of faulting, and
+// ycx_debug_bounds() returns the count. Release builds compile the test away.
+// One counter per translation unit (no relocatable device code); the host side sums them.
+#ifdef YCX_DEBUG_BOUNDS
+static __device__ unsigned int g_ycx_oob[2];  // [0] violations, [1] first line
+__device__ __forceinline__ bool ycx_bounds_ok(bool ok, int line) {
+  if (!ok && atomicAdd(&g_ycx_oob[0], 1u) == 0) atomicExch(&g_ycx_oob[1], (unsigned)line);
+  return ok;
+}
+#define YCX_BOUNDS_OK(lo, n, lim) ycx_bounds_ok((long long)(lo) >= 0 && (long long)(lo) + (n) <= (long long)(lim), __LINE__)
+// host: read (and optionally reset) this unit's counters
+#define YCX_DEFINE_BOUNDS_READER(fn)                                              \
+  ycx_status fn(unsigned* out, int reset) {                                      \
+    unsigned v[2] = {0, 0};                                                      \
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_ycx_oob), sizeof v) != hipSuccess)   \
+      return YCX_ERR_LAUNCH;                                                     \
+    out[0] += v[0];                                                              \
+    if (v[0] && !out[1]) out[1] = v[1];                                          \
+    if (reset) {                                                                 \
+      const unsigned z[2] = {0, 0};                                              \
+      if (hipMemcpyToSymbol(HIP_SYMBOL(g_ycx_oob), z, sizeof z) != hipSuccess)   \
+        return YCX_ERR_LAUNCH;                                                   \
+    }                                                                            \
+    return YCX_OK;                                                               \
+  }
+#else
+#define YCX_BOUNDS_OK(lo, n, lim) true
+#endif
+
 // Activation applied in the conv epilogues (Conv.act, nets/common.py:103).
 // FAST (bf16 outputs): the raw v_exp_f32 (2^x, no range fix-up: overflow to
 // inf gives rcp 0, i.e. silu -> 0) and v_rcp_f32, ~1 ulp fp32, far below bf16

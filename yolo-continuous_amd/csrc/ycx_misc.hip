@@ -9,6 +9,9 @@
 // threads take consecutive channel chunks of one pixel, so every wave reads and
 // writes whole contiguous channel rows.
 #include <vector>
+#include <rocprofiler-sdk-roctx/roctx.h>
+#include <stdio.h>
+
 #include "ycx_internal.h"
 
 namespace {
@@ -437,13 +440,38 @@ static ycx_status run_one(const ycx_op& op, void* stream) {
   }
 }
 
+// roctx ranges per op (SURVEY §5 tracing): off unless ycx_set_trace(1). One range per
+// op names its index, kind, kernel tile and shape, so a `rocprofv3 --marker-trace`
+// timeline of an eager forward lines each kernel up with its Model.forward layer.
+// (A HIP-graph replay has no host loop: trace an eager run.)
+static int g_trace = 0;
+
+extern "C" void ycx_set_trace(int32_t on) { g_trace = on != 0; }
+
+static void trace_push(int32_t i, const ycx_op& op) {
+  static const char* kinds[] = {"?", "conv", "stem", "pool", "copy", "stem2", "head"};
+  const char* k = (op.kind >= 1 && op.kind <= 6) ? kinds[op.kind] : kinds[0];
+  char buf[160];
+  if (op.kind == YCX_OP_CONV || op.kind == YCX_OP_STEM || op.kind == YCX_OP_HEAD || op.kind == YCX_OP_STEM2) {
+    const ycx_conv_desc& c = op.kind == YCX_OP_HEAD ? op.d.head.conv : op.kind == YCX_OP_STEM2 ? op.d.pair[1] : op.d.conv;
+    snprintf(buf, sizeof buf, "op%d %s %s n%d %dx%d %d->%d k%d s%d", i, k,
+             op.kind == YCX_OP_CONV ? ycx_conv_tile_name(c.tile ? c.tile : ycx_conv_pick_tile(&c)) : "", c.n, c.h,
+             c.w, c.cin, c.cout, c.kh, c.stride);
+  } else {
+    snprintf(buf, sizeof buf, "op%d %s", i, k);
+  }
+  roctxRangePushA(buf);
+}
+
 extern "C" ycx_status ycx_run_ops(const ycx_op* ops, int32_t n_ops, void* stream, void* const* events) {
   YCX_CHECK_ARG(ops && n_ops >= 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   for (int32_t i = 0; i < n_ops; ++i) {
     if (events && hipEventRecord(reinterpret_cast<hipEvent_t>(events[i]), st) != hipSuccess)
       return YCX_ERR_LAUNCH;
+    if (g_trace) trace_push(i, ops[i]);
     ycx_status s = run_one(ops[i], stream);
+    if (g_trace) roctxRangePop();
     if (s != YCX_OK) return s;
   }
   if (events && hipEventRecord(reinterpret_cast<hipEvent_t>(events[n_ops]), st) != hipSuccess)
@@ -483,6 +511,24 @@ extern "C" ycx_status ycx_graph_destroy(void* graph_exec) {
   YCX_CHECK_ARG(graph_exec);
   return hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(graph_exec)) == hipSuccess ? YCX_OK
                                                                                          : YCX_ERR_LAUNCH;
+}
+
+#ifdef YCX_DEBUG_BOUNDS
+extern "C" ycx_status ycx_dbg_bounds_conv(unsigned*, int);
+extern "C" ycx_status ycx_dbg_bounds_conv_f16(unsigned*, int);
+#endif
+
+extern "C" ycx_status ycx_debug_bounds(uint32_t* out, int32_t reset) {
+  YCX_CHECK_ARG(out);
+  out[0] = out[1] = 0;
+#ifdef YCX_DEBUG_BOUNDS
+  ycx_status s = ycx_dbg_bounds_conv(out, reset);
+  if (s == YCX_OK) s = ycx_dbg_bounds_conv_f16(out, reset);
+  return s;
+#else
+  (void)reset;
+  return YCX_ERR_UNSUPPORTED;  // a release build: the store checks are compiled out
+#endif
 }
 
 extern "C" int ycx_abi_version(void) { return YCX_ABI_VERSION; }

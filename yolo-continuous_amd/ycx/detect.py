@@ -318,8 +318,8 @@ class Detector:
             self._post.level_descs, self.cand, self.cand_rows, self.counts, keep_heads=keep_heads)
         self._post.fused = self.fused
         self.keep_heads = keep_heads or not self.fused
-        self.use_graph = use_graph
-        if use_graph:
+        self.use_graph = use_graph and not L.TRACE
+        if self.use_graph:
             self.engine.capture()
 
     def post(self):
