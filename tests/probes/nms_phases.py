@@ -8,7 +8,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("YCX_LIB", os.path.join(REPO, "yolo-continuous_amd", "csrc", "build", "libycx_hip_prof.so"))
+os.environ.setdefault("YCX_LIB", os.path.join(REPO, "yolo-continuous_amd", "ycx", "libycx_hip_prof.so"))
 sys.path[:0] = [REPO, os.path.join(REPO, "yolo-continuous_amd")]
 
 import torch  # noqa: E402

@@ -716,12 +716,483 @@ __device__ __forceinline__ int block_exclusive(int v, int* s_w, int* total) {
 }
 
 // ---------------------------------------------------------------------------
+// nms_big fast path: a class of S <= kFastMax boxes held entirely in LDS.
+// Same greedy semantics and the same suppressor / fixed-point logic as the
+// general path (resolve), with three changes that cut the per-class cost:
+//  * every candidate is gathered from global memory ONCE (into registers), and
+//    the rank sort, extent, histogram and scatter work from those registers
+//    (the general path re-gathers ci[bucket[r]] in each of four passes);
+//  * a finer grid per size level (4 << L cells a side, capped at 64: cells of
+//    1/4 - 1/2 of the level's box size instead of 1 - 2) and a tighter window:
+//    IoU > t forces the overlap width above t * max(w_i, w_j) (inter <= ox *
+//    min(h_i, h_j), union >= max(a_i, a_j)), so |cx_i - cx_j| < (w_i + w_j) / 2 -
+//    t * max(w_i, w_j), maximised over the partner level's width range [nw, mw]
+//    (the bound is piecewise linear in w_j with its kink at w_i); likewise in y.
+//    On the bench load this visits 3-4x fewer candidates (tools/nms_study.py);
+//  * after the search the suppressor lists move into LDS (CSR over the dead
+//    box region) so the fixed-point rounds never touch global memory.
+// Keys carry (row << 13 | e): e < 8192 is the element's load slot, so after the
+// sort every rank finds its box in the loading thread's registers.
+// ---------------------------------------------------------------------------
+constexpr int kFastMax = 8192;
+constexpr int kFLevels = 7;
+__host__ __device__ constexpr int fgrid(int L) { return (4 << L) < 64 ? (4 << L) : 64; }
+__host__ __device__ constexpr int fbase(int L) { return L == 0 ? 0 : fbase(L - 1) + fgrid(L - 1) * fgrid(L - 1); }
+constexpr int kFWild = fbase(kFLevels);  // boxes without a finite positive extent
+constexpr int kFCells = kFWild + 1;
+constexpr int kFCellBytes = ((kFCells + 1) / 2 * 4 + 255) & ~255;  // u16 end positions, packed in u32 words
+
+// LDS bytes of the fast path for a class of S boxes (cells, boxes, u16 ranks, state)
+__host__ __device__ inline int fast_lds_bytes(int S) { return kFCellBytes + 16 * S + ((2 * S + 15) & ~15) + S; }
+
+struct FGeo {
+  float cx, cy, w, h;
+  int level, cell;
+};
+
+__device__ __forceinline__ FGeo fgeometry(const f32x4 b, float X0, float Y0, float inv, bool all_pairs) {
+  FGeo g;
+  const float nx1 = (b[0] - X0) * inv, ny1 = (b[1] - Y0) * inv;
+  const float nx2 = (b[2] - X0) * inv, ny2 = (b[3] - Y0) * inv;
+  g.w = nx2 - nx1;
+  g.h = ny2 - ny1;
+  g.cx = (nx1 + nx2) * 0.5f;
+  g.cy = (ny1 + ny2) * 0.5f;
+  const float s = fmaxf(g.w, g.h);
+  const bool reg = !all_pairs && g.w > 0.0f && g.h > 0.0f && s < INFINITY && b[0] > -INFINITY && b[1] > -INFINITY;
+  if (!reg) {
+    g.level = -1;
+    g.cell = kFWild;
+    return g;
+  }
+  const int e = (int)(__float_as_uint(s) >> 23) - 126;  // s < 2^e
+  const int L = min(max(-e, 0), kFLevels - 1);
+  const int G = fgrid(L);
+  g.level = L;
+  g.cell = fbase(L) + clamp_cell(g.cy * (float)G, G) * G + clamp_cell(g.cx * (float)G, G);
+  return g;
+}
+
+// max over w_j in [nw, mw] of (w_i + w_j) / 2 - t max(w_i, w_j): the largest centre
+// distance at which a partner of that width range can still pass IoU > t
+__device__ __forceinline__ float reach(float wi, float nw, float mw, float t) {
+  auto f = [&](float wj) { return 0.5f * (wi + wj) - t * fmaxf(wi, wj); };
+  return fmaxf(fmaxf(f(nw), f(mw)), f(fminf(fmaxf(wi, nw), mw)));
+}
+
+__device__ __forceinline__ int u16_at(const unsigned* w, int k) { return (int)((w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu); }
+__device__ __forceinline__ int fcell_start(const unsigned* w, int k) { return k ? u16_at(w, k - 1) : 0; }
+
+// Position ranges [q0, q1) of the spatial order that can hold a suppressor of the
+// box of geometry g (as for_ranges, with the fast path's grid and tight window).
+template <class F>
+__device__ __forceinline__ void f_ranges(const unsigned* cells, const int (*lv)[5], const FGeo& g, int S,
+                                         float t_lo, float inv_t, F&& run) {
+  if (g.level < 0) {
+    run(0, S);
+    return;
+  }
+  run(fcell_start(cells, kFWild), u16_at(cells, kFWild));
+  constexpr float kSlack = 1e-6f, kEps = 1e-5f;
+  for (int L = 0; L < kFLevels; ++L) {
+    if (lv[L][0] == 0) continue;
+    const float mw = __int_as_float(lv[L][1]), mh = __int_as_float(lv[L][2]);
+    const float nw = __int_as_float(lv[L][3]), nh = __int_as_float(lv[L][4]);
+    if (mw + kSlack < t_lo * g.w || mh + kSlack < t_lo * g.h) continue;  // all too narrow / too flat
+    if (nw - kSlack > (g.w + kSlack) * inv_t || nh - kSlack > (g.h + kSlack) * inv_t) continue;  // too big
+    const int G = fgrid(L), base = fbase(L);
+    const float Gf = (float)G;
+    const float rx = reach(g.w, nw, mw, t_lo) + kEps, ry = reach(g.h, nh, mh, t_lo) + kEps;
+    const int ix0 = clamp_cell((g.cx - rx) * Gf, G), ix1 = clamp_cell((g.cx + rx) * Gf, G);
+    const int iy0 = clamp_cell((g.cy - ry) * Gf, G), iy1 = clamp_cell((g.cy + ry) * Gf, G);
+    for (int iy = iy0; iy <= iy1; ++iy) {  // cells ix0..ix1 of a grid row are contiguous positions
+      const int k0 = base + iy * G + ix0, k1 = base + iy * G + ix1;
+      run(fcell_start(cells, k0), u16_at(cells, k1));
+    }
+  }
+}
+
+// The fast path caches 32 suppressor ranks per box as u16 (the same 64 bytes per row
+// as the general path's 16 ints): past 32 it keeps the 32 highest-ranked, found with
+// one 64-byte read, so a box rarely needs a rescan and the search never walks a
+// dependent chain of global loads.
+constexpr int kFSlots = 32;
+
+// f(k, v) for the first c of a box's u16 slots, read as 16-byte chunks (4 registers live)
+template <class F>
+__device__ __forceinline__ void for_slots16(const unsigned short* sl, int c, F&& f) {
+  const int4* s4 = reinterpret_cast<const int4*>(sl);
+  for (int q = 0; q < (c + 7) / 8; ++q) {
+    const int4 x = s4[q];
+    const int w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int h = 0; h < 8; ++h)
+      if (8 * q + h < c) f(8 * q + h, (int)(((unsigned)w[h >> 1] >> (16 * (h & 1))) & 0xFFFFu));
+  }
+}
+
+// the rare replacement past kFSlots: keep the kFSlots highest-ranked (smallest ranks)
+__device__ __forceinline__ void replace_slot16(unsigned short* sl, int rj) {
+  int km = 0, vm = -1;
+  for_slots16(sl, kFSlots, [&](int k, int v) {
+    km = v > vm ? k : km;
+    vm = v > vm ? v : vm;
+  });
+  if (rj < vm) sl[km] = (unsigned short)rj;
+}
+
+template <int E>
+__device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restrict__ ci, const Ptrs& P, char* smem, int (*s_lv)[5],
+                         int* s_ext, int* s_w, int* s_flag, const Thr& thr, float t_lo, float inv_t, int all_pairs) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int S = tk.S, off = tk.off;
+  const int* bucket = P.bucket + off;
+#ifdef YCX_NMS_PROFILE
+  unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
+#endif
+  __syncthreads();  // s_ext / s_lv initialised
+  // (1) sort keys of elements e = tid * E + i (score desc, row asc; e in the low bits)
+  unsigned long long key[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = tid * E + i;
+    const int row = e < S ? bucket[e] : -1;
+    if (row >= 0) {
+      const ycx_cand& c = ci[row];
+      const float score = c.obj * c.cls_conf;
+      key[i] = ((unsigned long long)(0xFFFFFFFFu - __float_as_uint(score)) << 32) | ((unsigned)row << 13) | (unsigned)e;
+    } else {
+      key[i] = ~0ull;
+    }
+  }
+  // (2) rank sort in registers (exchange through LDS), then every element learns its rank
+  unsigned long long* xch = reinterpret_cast<unsigned long long*>(smem);
+  unsigned short* rank_of = reinterpret_cast<unsigned short*>(smem + 8 * kFastMax);
+  sort_regs<E>(key, xch, E * kBigThreads);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < E; ++i)
+    if (tid * E + i < S) rank_of[key[i] & 0x1FFF] = (unsigned short)(tid * E + i);
+  __syncthreads();
+  int myrank[E];
+  f32x4 box[E];  // the elements' boxes, gathered again now that the keys are dead
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = tid * E + i;
+    myrank[i] = e < S ? rank_of[e] : 0;
+    if (e < S) {
+      const ycx_cand& c = ci[bucket[e]];
+      box[i] = f32x4{c.x1, c.y1, c.x2, c.y2};
+    } else {
+      box[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __syncthreads();  // every element's bucket entry read
+  int* rank_row = P.bucket + off;  // bucket in rank order from here
+#pragma unroll
+  for (int i = 0; i < E; ++i)
+    if (tid * E + i < S) rank_row[tid * E + i] = (int)((key[i] >> 13) & 0x7FFFF);
+
+  // class extent of the regular boxes (wave reduce, four LDS atomics per wave)
+  {
+    int mn0 = 0x7FFFFFFF, mn1 = 0x7FFFFFFF, mx2 = (int)0x80000000, mx3 = (int)0x80000000;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const f32x4 b = box[i];
+      if (tid * E + i < S && b[2] > b[0] && b[3] > b[1] && b[0] > -INFINITY && b[1] > -INFINITY && b[2] < INFINITY &&
+          b[3] < INFINITY) {
+        mn0 = min(mn0, f2o(b[0]));
+        mn1 = min(mn1, f2o(b[1]));
+        mx2 = max(mx2, f2o(b[2]));
+        mx3 = max(mx3, f2o(b[3]));
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mn0 = min(mn0, __shfl_xor(mn0, o));
+      mn1 = min(mn1, __shfl_xor(mn1, o));
+      mx2 = max(mx2, __shfl_xor(mx2, o));
+      mx3 = max(mx3, __shfl_xor(mx3, o));
+    }
+    if (lane == 0) {
+      atomicMin(&s_ext[0], mn0);
+      atomicMin(&s_ext[1], mn1);
+      atomicMax(&s_ext[2], mx2);
+      atomicMax(&s_ext[3], mx3);
+    }
+  }
+  __syncthreads();  // rank_of dead: LDS becomes the cell table + boxes; extent complete
+  YCX_PROF_MARK(0)
+  // (3) spatial counting sort on the fine grid
+  unsigned* cells = reinterpret_cast<unsigned*>(smem);
+  for (int k = tid; k < kFCellBytes / 4; k += kBigThreads) cells[k] = 0;
+  __syncthreads();
+  const float X0 = o2f(s_ext[0]), Y0 = o2f(s_ext[1]);
+  const float Ex = fmaxf(o2f(s_ext[2]) - X0, o2f(s_ext[3]) - Y0);
+  const float inv = (Ex > 0.0f && Ex < INFINITY) ? 1.0f / Ex : 0.0f;  // 0: every box irregular
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    if (tid * E + i < S) {
+      const int k = fgeometry(box[i], X0, Y0, inv, all_pairs).cell;
+      atomicAdd(&cells[k >> 1], 1u << ((k & 1) * 16));
+    }
+  }
+  // per-level count / extreme sizes: wave-reduced, one LDS atomic per wave and level
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    FGeo g;
+    g.level = -1;
+    if (tid * E + i < S) g = fgeometry(box[i], X0, Y0, inv, all_pairs);
+    for (int Lv = 0; Lv < kFLevels; ++Lv) {
+      const bool in = g.level == Lv;
+      const unsigned long long m = __ballot(in);
+      if (!m) continue;
+      int mxw = in ? __float_as_int(g.w) : 0, mxh = in ? __float_as_int(g.h) : 0;
+      int mnw = in ? __float_as_int(g.w) : 0x7F800000, mnh = in ? __float_as_int(g.h) : 0x7F800000;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        mxw = max(mxw, __shfl_xor(mxw, o));
+        mxh = max(mxh, __shfl_xor(mxh, o));
+        mnw = min(mnw, __shfl_xor(mnw, o));
+        mnh = min(mnh, __shfl_xor(mnh, o));
+      }
+      if (lane == 0) {
+        atomicAdd(&s_lv[Lv][0], __popcll(m));
+        atomicMax(&s_lv[Lv][1], mxw);
+        atomicMax(&s_lv[Lv][2], mxh);
+        atomicMin(&s_lv[Lv][3], mnw);
+        atomicMin(&s_lv[Lv][4], mnh);
+      }
+    }
+  }
+  __syncthreads();
+  {  // exclusive scan of the u16 counts, in place: each thread a contiguous run of cells
+    constexpr int kPer = (kFCells + kBigThreads - 1) / kBigThreads;
+    const int c0 = tid * kPer, c1 = min(kFCells, c0 + kPer);
+    int s = 0;
+    for (int k = c0; k < c1; ++k) s += u16_at(cells, k);
+    int total;
+    int run = block_exclusive(s, s_w, &total);
+    __syncthreads();  // every count read before any is overwritten
+    unsigned short* c16 = reinterpret_cast<unsigned short*>(cells);
+    for (int k = c0; k < c1; ++k) {
+      const int v = c16[k];
+      c16[k] = (unsigned short)run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  f32x4* lbox = reinterpret_cast<f32x4*>(smem + kFCellBytes);
+  unsigned short* lr = reinterpret_cast<unsigned short*>(smem + kFCellBytes + 16 * S);
+  unsigned char* st = reinterpret_cast<unsigned char*>(smem + kFCellBytes + 16 * S + ((2 * S + 15) & ~15));
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    if (tid * E + i >= S) continue;
+    const int k = fgeometry(box[i], X0, Y0, inv, all_pairs).cell;
+    const unsigned old = atomicAdd(&cells[k >> 1], 1u << ((k & 1) * 16));  // ends as the end of cell k
+    const int q = (int)((old >> ((k & 1) * 16)) & 0xFFFFu);
+    lbox[q] = box[i];
+    lr[q] = (unsigned short)myrank[i];
+    P.sbox[off + q] = box[i];  // global copies for the rare rescan after the boxes' LDS is reused
+    P.srank[off + q] = myrank[i];
+  }
+  __syncthreads();
+  YCX_PROF_MARK(1)
+  // (4) suppressors of every box (spatial order), kSlots highest-ranked kept (global slots)
+  for (int p = tid; p < S; p += kBigThreads) {
+    const int r = lr[p];
+    const f32x4 b = lbox[p];
+    const float a = box_area(b);
+    const FGeo g = fgeometry(b, X0, Y0, inv, all_pairs);
+    unsigned short* sl = reinterpret_cast<unsigned short*>(P.slots + (size_t)(off + p) * kSlots);
+    int ns = 0;
+#ifdef YCX_NMS_PROFILE
+    int visits = 0;
+#endif
+    auto test = [&](int rj, const f32x4& o) {
+      const bool cand = rj < r && (all_pairs || (o[0] < b[2] && o[2] > b[0] && o[1] < b[3] && o[3] > b[1]));
+      if (cand && suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
+        if (ns < kFSlots) {
+          sl[ns] = (unsigned short)rj;
+        } else {  // rare: keep the kFSlots highest-ranked (smallest ranks)
+          replace_slot16(sl, rj);
+        }
+        ++ns;
+      }
+    };
+    f_ranges(cells, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
+#ifdef YCX_NMS_PROFILE
+      visits += q1 - q0;
+#endif
+      int q = q0;
+      for (; q + 4 <= q1; q += 4) {
+        int rj[4];
+        f32x4 o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          rj[u] = lr[q + u];
+          o[u] = lbox[q + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) test(rj[u], o[u]);
+      }
+      for (; q < q1; ++q) test(lr[q], lbox[q]);
+    });
+    P.nsup[off + p] = ns;
+#ifdef YCX_NMS_PROFILE
+    if (ns > kFSlots) atomicAdd(&g_nms_prof[6], 1ull);
+    atomicAdd(&g_nms_prof[8], (unsigned long long)visits);
+    atomicAdd(&g_nms_prof[10], (unsigned long long)ns);
+    int mx = visits;
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+    if (lane == 0) atomicAdd(&g_nms_prof[9], (unsigned long long)mx);
+#endif
+  }
+  for (int r = tid; r < S; r += kBigThreads) st[r] = 0;
+  // (5) suppressor lists into LDS (CSR over the dead box region), if they fit
+  __syncthreads();  // every search read of lbox done: its region becomes the CSR
+  unsigned* csr_off = reinterpret_cast<unsigned*>(lbox);                     // [S]
+  unsigned short* csr_ns = reinterpret_cast<unsigned short*>(csr_off + S);  // [S] min(ns, 0xFFFF)
+  unsigned short* csr = csr_ns + ((S + 1) & ~1);                             // [total]
+  int my_total = 0;  // positions p = tid + k * kBigThreads (the search's own: its nsup writes are this thread's)
+  for (int p = tid; p < S; p += kBigThreads) my_total += min(P.nsup[off + p], kFSlots);
+  int total;
+  int base = block_exclusive(my_total, s_w, &total);
+  const bool lds_csr = 4 * S + 2 * ((S + 1) & ~1) + 2 * total <= 16 * S;
+  if (lds_csr) {
+    for (int p = tid; p < S; p += kBigThreads) {
+      const int ns = P.nsup[off + p], c = min(ns, kFSlots);
+      for_slots16(reinterpret_cast<const unsigned short*>(P.slots + (size_t)(off + p) * kSlots), c,
+                  [&](int k, int v) { csr[base + k] = (unsigned short)v; });
+      csr_off[p] = base;
+      csr_ns[p] = (unsigned short)min(ns, 0xFFFF);
+      base += c;
+    }
+  }
+  __syncthreads();
+  YCX_PROF_MARK(2)
+  // (6) greedy as a fixed point over ranks: 0 undecided, 1 kept, 2 removed
+  for (int it = 0; it <= S; ++it) {  // every round decides at least one box
+    if (tid == 0) *s_flag = 0;
+    __syncthreads();
+    int undecided = 0;
+    for (int p = tid; p < S; p += kBigThreads) {
+      const int r = lr[p];
+      if (st[r] != 0) continue;
+      int ns, res = 0;  // 0: every suppressor removed, 1: some undecided, 2: one kept
+      if (lds_csr) {
+        ns = csr_ns[p];
+        const int b0 = csr_off[p], c = min(ns, kFSlots);
+        for (int k = 0; k < c && res != 2; ++k) {
+          const unsigned char sj = st[csr[b0 + k]];
+          res = sj == 1 ? 2 : (sj == 0 ? 1 : res);
+        }
+      } else {
+        ns = P.nsup[off + p];
+        for_slots16(reinterpret_cast<const unsigned short*>(P.slots + (size_t)(off + p) * kSlots), min(ns, kFSlots),
+                    [&](int, int v) {
+                      const unsigned char sj = st[v];
+                      res = res == 2 ? 2 : (sj == 1 ? 2 : (sj == 0 ? 1 : res));
+                    });
+      }
+      if (ns > kFSlots && res == 0) {  // the cached ones are all removed: rescan (global copies)
+        const f32x4 b = P.sbox[off + p];
+        const float a = box_area(b);
+        const FGeo g = fgeometry(b, X0, Y0, inv, all_pairs);
+        bool stop = false;
+        f_ranges(cells, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
+          for (int q = q0; q < q1 && !stop; ++q) {
+            const int rj = P.srank[off + q];
+            if (rj >= r) continue;
+            const unsigned char sj = st[rj];
+            if (sj == 2) continue;
+            const f32x4 o = P.sbox[off + q];
+            if (suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
+              if (sj == 1) { res = 2; stop = true; }
+              else res = 1;
+            }
+          }
+        });
+      }
+      if (res == 2) st[r] = 2;
+      else if (res == 0) st[r] = 1;
+      else undecided = 1;
+    }
+    if (undecided) *s_flag = 1;
+    __syncthreads();
+    const int more = *s_flag;
+    __syncthreads();
+#ifdef YCX_NMS_PROFILE
+    if (tid == 0) atomicAdd(&g_nms_prof[5], 1ull);
+#endif
+    if (!more) break;
+  }
+  YCX_PROF_MARK(3)
+  // (7) kept rows in rank order: thread tid takes ranks tid * E .. + E - 1
+  int nk = 0;
+#pragma unroll
+  for (int i = 0; i < E; ++i) nk += (tid * E + i < S && st[tid * E + i] == 1) ? 1 : 0;
+  int kt;
+  int pos = block_exclusive(nk, s_w, &kt);
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int r = tid * E + i;
+    if (r < S && st[r] == 1) P.kept[off + pos++] = rank_row[r];
+  }
+  if (tid == 0) P.kc[tk.cls] = kt;
+  __syncthreads();
+  YCX_PROF_MARK(4)
+}
+
+// ---------------------------------------------------------------------------
+// The LDS-resident classes (S <= kFastMax and fast_lds_bytes(S) fits): big_fast, one
+// 1024-thread workgroup per class (grid-strided task loop); nms_big then takes the rest.
+template <int E>  // one launch per register-array width: each instance allocates its own registers
+__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_fast(
+    ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws, Thr thr, float t_lo, float inv_t, int all_pairs) {
+  __shared__ __attribute__((aligned(16))) char smem[kBigLds];
+  __shared__ int s_lv[kFLevels][5];
+  __shared__ int s_ext[4];
+  __shared__ int s_w[kBigThreads / 64];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x;
+  const int rows = d.rows_total;
+  const Layout L = layout(d.n, rows);
+  const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
+  const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks);
+  const int ntasks = hdr->ntasks;
+  for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
+    const Task tk = tasks[t];
+    const int S = tk.S;
+    if (!(S <= kFastMax && fast_lds_bytes(S) <= kBigLds)) continue;  // nms_big's task (uniform)
+    if (max(next_pow2(S), kBigThreads) / kBigThreads != E) continue;  // another width's launch
+    const Ptrs P = image_ptrs(ws, L, tk.img);
+    const ycx_cand* ci = cand + (size_t)tk.img * rows;
+#ifdef YCX_NMS_PROFILE
+    if (tid == 0) atomicAdd(&g_nms_prof[7], 1ull);
+#endif
+    if (tid == 0) {
+      s_ext[0] = s_ext[1] = 0x7FFFFFFF;  // min x1, min y1
+      s_ext[2] = s_ext[3] = (int)0x80000000;  // max x2, max y2
+    }
+    if (tid < kFLevels) {
+      s_lv[tid][0] = 0;
+      s_lv[tid][1] = s_lv[tid][2] = 0;  // +0.0f
+      s_lv[tid][3] = s_lv[tid][4] = 0x7F800000;  // +inf
+    }
+    big_fast<E>(tk, ci, P, smem, s_lv, s_ext, s_w, &s_flag, thr, t_lo, inv_t, all_pairs);
+  }
+}
+
+// ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_big(ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws,
                                                     Thr thr, float t_lo, float inv_t, int all_pairs) {
   constexpr int kLdsBytes = kBigLds;
   constexpr int kLdsCellBytes = ((kCells * 4) + 255) & ~255;
   // register sorts exchange through LDS when the keys fit (Pn <= kLdsBytes / 8), else the workspace
   static_assert(kLdsBytes >= 8 * kBigThreads * 8 && kLdsBytes >= ((kCells * 4 + 255) & ~255) + 1024, "LDS budget");
+  static_assert(kLdsBytes >= 10 * kFastMax, "fast path: sort exchange + rank table");
+  static_assert(kFSlots * 2 == kSlots * 4 && kFastMax <= 65536, "fast path: u16 slots in the general path's rows");
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
   __shared__ int s_lv[kLevels][5];
   __shared__ int s_ext[4];
@@ -740,6 +1211,9 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
     const ycx_cand* ci = cand + (size_t)tk.img * rows;
     const int S = tk.S, off = tk.off;
     int* bucket = P.bucket + off;
+#ifndef YCX_NMS_NO_FAST
+    if (S <= kFastMax && fast_lds_bytes(S) <= kLdsBytes) continue;  // nms_fast's task (uniform)
+#endif
 #ifdef YCX_NMS_PROFILE
     unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
     if (tid == 0) atomicAdd(&g_nms_prof[7], 1ull);
@@ -753,8 +1227,8 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
       s_lv[tid][1] = s_lv[tid][2] = 0;  // +0.0f
       s_lv[tid][3] = s_lv[tid][4] = 0x7F800000;  // +inf
     }
-    // (1) rank = position in (score desc, row asc) order
     const int Pn = max(next_pow2(S), kBigThreads);
+    // (1) rank = position in (score desc, row asc) order
     unsigned long long* keys =
         Pn <= kLdsBytes / 8 ? reinterpret_cast<unsigned long long*>(smem) : P.keys + 2 * (size_t)off;
     switch (Pn / kBigThreads) {  // uniform
@@ -969,6 +1443,12 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   const float t_lo = all_pairs ? 0.0f : (float)(fmin(d->iou_thres, 1.0) * (1.0 - 1e-3));
   const float inv_t = t_lo > 0.0f ? 1.0f / t_lo : INFINITY;
   hipLaunchKernelGGL(nms_prep, dim3(d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws, t);
+#ifndef YCX_NMS_NO_FAST
+  hipLaunchKernelGGL(nms_fast<8>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
+  hipLaunchKernelGGL(nms_fast<4>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
+  hipLaunchKernelGGL(nms_fast<2>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
+  hipLaunchKernelGGL(nms_fast<1>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
+#endif
   hipLaunchKernelGGL(nms_big, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
   hipLaunchKernelGGL(nms_finish, dim3(d->n), dim3(kThreads), 0, st, *d, cand, ws, dets, keep_rows, keep_counts);
   return ycx_launch_status();
