@@ -26,6 +26,18 @@ def main():
     det()
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * 16)()
+    prof = hasattr(L.lib, "ycx_nms_prof_read")  # False on the release library: post time only
+    if not prof:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        det.forward()
+        e0.record()
+        for _ in range(5):
+            det.post()
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"release library: post ms {e0.elapsed_time(e1) / 5:.3f}")
+        return
+    L.lib.ycx_nms_prof_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.lib.ycx_nms_prof_read(buf, 1)
     reps = 3
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -44,6 +56,8 @@ def main():
     nt = max(1, buf[7])
     print(f"  candidate visits/task {buf[8] / nt:.0f}  sum of per-wave max visits x64/task {64 * buf[9] / nt:.0f}  "
           f"suppressor pairs/task {buf[10] / nt:.0f}")
+    print(f"  search: mean wave {buf[11] / (16 * nt) / 1e3:.1f} kcycles, slowest wave {buf[12] / nt / 1e3:.1f} kcycles, "
+          f"slowest wave's visits {buf[13] / nt:.0f} (mean {buf[8] / (16 * nt):.0f})")
     cnt = det.counts.cpu()
     print("candidates/img", cnt.float().mean().item())
     ws = det.ws.view(torch.int32).cpu()  # header (ntasks) then the task table {img, cls, off, S} at byte 256

@@ -73,7 +73,8 @@ def _run_conv(device, n, h, w, cin, cout, k, s, act, tile, dtype, in_extra=0, ou
 TILES_BF16 = [(1, 128, 64), (2, 64, 64), (3, 64, 64), (4, 128, 64), (5, 32, 32), (6, 64, 32), (7, 128, 32),
               (9, 128, 64), (10, 64, 64), (11, 256, 128), (12, 128, 64), (13, 64, 32), (14, 128, 32), (14, 256, 32),
               (15, 64, 64), (16, 128, 64), (17, 64, 32), (18, 64, 128), (40, 256, 64), (40, 256, 32),
-              (40, 512, 96)]
+              (40, 512, 96), (41, 256, 64), (41, 512, 96), (42, 128, 64), (42, 256, 32), (43, 128, 64),
+              (43, 256, 96)]
 
 
 @pytest.mark.parametrize('tile,cout,cin', TILES_BF16)
@@ -87,7 +88,8 @@ def test_conv_bf16_tiles(device, tile, cout, cin, k, s):
 @pytest.mark.parametrize('tile,cout,cin,k,s', [(16, 128, 64, 3, 1), (16, 256, 128, 1, 1), (18, 64, 128, 3, 2),
                                                (17, 64, 32, 3, 1), (5, 32, 32, 3, 1), (7, 128, 32, 3, 2),
                                                (1, 128, 64, 3, 1), (11, 256, 128, 3, 1), (40, 256, 64, 3, 1),
-                                               (40, 512, 128, 1, 1)])
+                                               (40, 512, 128, 1, 1), (41, 256, 64, 3, 1), (42, 128, 64, 1, 1),
+                                               (43, 256, 128, 3, 2)])
 def test_conv_fp16_tiles(device, tile, cout, cin, k, s):
     """The same tiles built with IEEE half elements (YCX_DT_F16, v_mfma_f32_16x16x32_f16):
     fp16 output rounding (2^-11 relative) on top of exact products of fp16 inputs."""
@@ -155,16 +157,17 @@ def test_conv3x3_ws64(device, n, hw, cout, act):
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
 
 
-def test_conv_big_tile_residual_up2_slices(device):
-    """Tile 40 (256 x 256 x 32, four stages): residual add, x2 upsample store, channel
+@pytest.mark.parametrize('tile', [40, 41, 42, 43])
+def test_conv_big_tile_residual_up2_slices(device, tile):
+    """Tiles 40-43 (conv_bigt, 32-deep K stages): residual add, x2 upsample store, channel
     slices, a ragged pixel tail over several workgroups (M = 2 * 23 * 19 = 874)."""
-    got, ref = _run_conv(device, 2, 23, 19, 128, 256, 3, 1, L.ACT_LEAKY, 40, L.DT_BF16, residual=True,
+    got, ref = _run_conv(device, 2, 23, 19, 128, 256, 3, 1, L.ACT_LEAKY, tile, L.DT_BF16, residual=True,
                          in_extra=8)
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=2e-2)
-    got, ref = _run_conv(device, 2, 23, 19, 64, 512, 1, 1, L.ACT_SILU, 40, L.DT_BF16, layout=L.OUT_NHWC_UP2,
+    got, ref = _run_conv(device, 2, 23, 19, 64, 512, 1, 1, L.ACT_SILU, tile, L.DT_BF16, layout=L.OUT_NHWC_UP2,
                          out_extra=8)
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
-    got, ref = _run_conv(device, 3, 20, 20, 256, 248, 3, 2, L.ACT_SILU, 40, L.DT_BF16, in_extra=16, out_extra=8)
+    got, ref = _run_conv(device, 3, 20, 20, 256, 248, 3, 2, L.ACT_SILU, tile, L.DT_BF16, in_extra=16, out_extra=8)
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
 
 

@@ -238,3 +238,30 @@ def test_detector_close_releases_its_engine(device):
     cd.submit(torch.zeros(shape, device=device))
     cd.close()
     assert len(m._engines) == base
+
+
+@pytest.mark.parametrize('precision', ['bf16', 'fp8'])
+def test_chunked_prefix_bit_identical(device, precision, monkeypatch):
+    """YCX_CHUNK='k:cut' (the image-chunked prefix experiment) runs the plan's first cut
+    ops k images at a time: every op is image-major, so the fused Detector's outputs
+    must equal the unchunked plan's bit for bit."""
+    from ycx.detect import Detector
+    m, _ = make_model('yolov7', 80, 0, precision)
+    m.to(device)
+    if precision == 'fp8':
+        m.calibrate_fp8(device=device, hw=(160, 160), n=2)
+    x = synthetic_images(4, 3, 160, 160, seed=5).to(device)
+    kw = dict(conf_thres=0.3, nms_thres=0.45, max_det=2000, keep_heads=True)
+    det = Detector(m, tuple(x.shape), device, ANCHORS, [[6, 7, 8], [3, 4, 5], [0, 1, 2]], **kw)
+    d0, k0, c0 = [t.clone() for t in det(x)]
+    h0 = [h.clone() for h in det.heads]
+    det.close()
+    monkeypatch.setenv('YCX_CHUNK', '2:40')
+    det = Detector(m, tuple(x.shape), device, ANCHORS, [[6, 7, 8], [3, 4, 5], [0, 1, 2]], **kw)
+    d1, k1, c1 = det(x)
+    torch.cuda.synchronize()
+    assert det.engine._exec_ops()[1] > det.engine.n_ops  # the chunked list really ran
+    for a, b in zip(h0, det.heads):
+        assert torch.equal(a, b)
+    assert torch.equal(c0, c1) and torch.equal(k0, k1) and torch.equal(d0, d1)
+    det.close()

@@ -3,7 +3,9 @@
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/r03
 cd $R
-CONV_SHAPES=0,2,5,10,12,14,16,18,20,22,23,26,27 timeout -k 10 300 python tests/probes/conv_bench.py 16 40 > gpurun_out/r03/conv_16_40.log 2>&1 || { tail -20 gpurun_out/r03/conv_16_40.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q -k "big or bf16_tiles or fp16_tiles" --timeout 200 --timeout-method thread > gpurun_out/r03/tiles_tests.log 2>&1 || { tail -30 gpurun_out/r03/tiles_tests.log; exit 1; }
+tail -1 gpurun_out/r03/tiles_tests.log
+CONV_SHAPES=0,2,5,10,12,14,16,18,20,22,23,26,27 timeout -k 10 300 python tests/probes/conv_bench.py 16 40 41 42 43 > gpurun_out/r03/conv_16_40.log 2>&1 || { tail -20 gpurun_out/r03/conv_16_40.log; exit 1; }
 cat gpurun_out/r03/conv_16_40.log
 for gc in 0 2 4; do
   echo "gc=$gc"

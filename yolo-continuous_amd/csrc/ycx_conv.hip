@@ -970,44 +970,69 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
 // the source side. A rows are permuted as in conv_bf16_glds so the epilogue stores 16
 // bytes per lane and pixel (epilogue_regs8: bias, act, residual, x2 upsample).
 // -------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) conv_big(ConvArgs a) {
-  constexpr int BM = 256, BN = 256, BK = 32, NS = 4, TM = 64, TN = 64, FM = 4, FN = 4;
-  constexpr int A_BYTES = BM * BK * 2, STAGE = 2 * A_BYTES;  // A then B, 16 KiB each
+// Generalised (r03): conv_bigt<BM, BN, WM, WN, NS>, waves of 64 x 64 or 64 x 32 fragments, 32-deep
+// K stages, NS stages in LDS with NS - 1 in flight; each wave DMAs BM / (16 NW) A pieces and
+// BN / (16 NW) B pieces (16 rows x 64 B) per stage. Tile 40 = <256, 256, 4, 4, 4>; 41 =
+// <256, 128, 4, 2, 3> and 42 = <128, 256, 2, 4, 3> (72 KiB, two workgroups per CU, 25 % fewer
+// bytes per FLOP than tile 16 and two stages in flight per workgroup); 43 = <128, 128, 2, 4, 4>
+// (tile 16's bytes per FLOP, three stages in flight: the pipelining depth alone).
+template <int NSUB>
+__device__ __forceinline__ void vm_wait_stages(int younger) {  // younger stages of NSUB DMAs per wave may stay
+  if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NSUB) : "memory");
+  else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NSUB) : "memory");
+  else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSUB) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int NS>
+__global__ void __launch_bounds__(WM * WN * 64) conv_bigt(ConvArgs a) {
+  constexpr int NW = WM * WN, BK = 32, TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_PW = BM / (16 * NW), B_PW = BN / (16 * NW), LPS = A_PW + B_PW;
+  static_assert(TM == 64 && (TN == 64 || TN == 32) && A_PW >= 1 && B_PW >= 1 && NS >= 2 && NS <= 4, "tile shape");
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
   const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
   const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
+  const int wm = wid / WN, wn = wid % WN;
   const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
-  const int ct = L % a.n_ct, pt = L / a.n_ct;
+  int ct, pt;
+  ycx_tile_of(L, a.n_ct, a.nwg / a.n_ct, a.gc, ct, pt);
   const int co0 = ct * BM, px0 = pt * BN;
-  const int row = 16 * wid + (lane >> 2), pch = lane & 3;  // this lane's DMA row (A and B) and LDS chunk
-  const int lch = pch ^ swz<BK>(row);                       // logical chunk it fetches
+  const int pch = lane & 3;
   const int w_bytes = a.Cout_pad * a.Ktot * 2, x_bytes = a.N * a.H * a.W * a.in_cs * 2;
-  int a_off;
-  {
+  int a_off[A_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int row = 16 * (wid + NW * i) + (lane >> 2);
     const int f = (row % TM) >> 4, m = row & 15;
     const int ch = (row / TM) * TM + 32 * (f >> 1) + 8 * (m >> 2) + 4 * (f & 1) + (m & 3);
-    a_off = ((co0 + ch) * a.Ktot + (lch << 3)) * 2;
+    a_off[i] = ((co0 + ch) * a.Ktot + ((pch ^ swz<BK>(row)) << 3)) * 2;
   }
-  int b_iy0, b_ix0, b_base;
-  {
+  int b_iy0[B_PW], b_ix0[B_PW], b_base[B_PW];
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int row = 16 * (wid + NW * i) + (lane >> 2);
     const int p = px0 + row;
     const bool ok = p < a.M;
     const int pp = ok ? p : 0;
     const int n = pp / a.HoWo, rem = pp - n * a.HoWo;
     const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
-    b_iy0 = ok ? oy * a.S - a.P : -(1 << 20);  // tail rows fail the bounds test: zeros
-    b_ix0 = ox * a.S - a.P;
-    b_base = (((n * a.H + b_iy0) * a.W + b_ix0) * a.in_cs + a.in_coff + (lch << 3)) * 2;
+    b_iy0[i] = ok ? oy * a.S - a.P : -(1 << 20);  // tail rows fail the bounds test: zeros
+    b_ix0[i] = ox * a.S - a.P;
+    b_base[i] = (((n * a.H + b_iy0[i]) * a.W + b_ix0[i]) * a.in_cs + a.in_coff + ((pch ^ swz<BK>(row)) << 3)) * 2;
   }
   int i_ky = 0, i_kx = 0, i_cb = 0;  // K position of the next stage to issue
   auto issue = [&](int s, int slot) {
     char* base = smem + slot * STAGE;
-    buf_lds16(Wt, w_bytes, a_off, s * (BK * 2), base + wid * 1024);
-    const bool ok = (unsigned)(b_iy0 + i_ky) < (unsigned)a.H && (unsigned)(b_ix0 + i_kx) < (unsigned)a.W;
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * (BK * 2), base + (wid + NW * i) * 1024);
     const int tap = ((i_ky * a.W + i_kx) * a.in_cs + i_cb) * 2;
-    buf_lds16(X, x_bytes, ok ? b_base + tap : 0x7FFFFFF0, 0, base + A_BYTES + wid * 1024);
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      const bool ok = (unsigned)(b_iy0[i] + i_ky) < (unsigned)a.H && (unsigned)(b_ix0[i] + i_kx) < (unsigned)a.W;
+      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + A_BYTES + (wid + NW * i) * 1024);
+    }
     i_cb += BK;
     if (i_cb == a.Cin) {
       i_cb = 0;
@@ -1024,11 +1049,8 @@ __global__ void __launch_bounds__(1024) conv_big(ConvArgs a) {
   for (int s = 0; s < NS - 1; ++s)
     if (s < nt) issue(s, s);
   for (int t = 0; t < nt; ++t) {
-    // two DMAs per stage and wave: stage t is complete once at most the younger stages remain
-    const int younger = min(NS - 2, nt - 1 - t);
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // stage t is complete once at most its younger stages' DMAs remain
+    vm_wait_stages<LPS>(min(NS - 2, nt - 1 - t));
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);  // the slot of stage t - 1, read by all
@@ -2908,6 +2930,9 @@ const TileInfo kTiles[] = {
     {256, 64, 64, "head_co256_px64_decode"},
     {256, 64, 128, "f8_head_co256_px64_decode"},
     {256, 256, 32, "big_co256_px256_k32_s4"},
+    {256, 128, 32, "big_co256_px128_k32_s3"},
+    {128, 256, 32, "big_co128_px256_k32_s3"},
+    {128, 128, 32, "big_co128_px128_k32_s4"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -2984,13 +3009,15 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
-// tile 40: conv_big (256 x 256 x 32, four stages, one 1024-thread workgroup per CU)
-ycx_status launch_big(ConvArgs a, hipStream_t st) {
-  if (a.Cin % 32 || a.Cout_pad % 256 || a.out_layout == YCX_OUT_NCHW_F32 || a.pool) return YCX_ERR_UNSUPPORTED;
+// tiles 40-43: conv_bigt (32-deep K stages, NS - 1 in flight)
+template <int BM, int BN, int WM, int WN, int NS>
+ycx_status launch_bigt(ConvArgs a, hipStream_t st) {
+  if (a.Cin % 32 || a.Cout_pad % BM || a.out_layout == YCX_OUT_NCHW_F32 || a.pool) return YCX_ERR_UNSUPPORTED;
   a.nsteps = a.KH * a.KW * (a.Cin / 32);
-  a.n_ct = a.Cout_pad / 256;
-  a.nwg = a.n_ct * ((a.M + 255) / 256);
-  hipLaunchKernelGGL(conv_big, dim3(a.nwg), dim3(1024), 0, st, a);
+  a.n_ct = a.Cout_pad / BM;
+  a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
+  a.gc = glds_gc(a);
+  hipLaunchKernelGGL((conv_bigt<BM, BN, WM, WN, NS>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
   return ycx_launch_status();
 }
 
@@ -3335,7 +3362,10 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x,
     case 24: return launch_glds<256, 256, 2, 4, false, 2>(a, st);
     case 25: return launch_glds<256, 128, 2, 4, false, 2>(a, st);
     case 26: return launch_glds<128, 256, 2, 4, false, 2>(a, st);
-    case 40: return launch_big(a, st);
+    case 40: return launch_bigt<256, 256, 4, 4, 4>(a, st);
+    case 41: return launch_bigt<256, 128, 4, 2, 3>(a, st);
+    case 42: return launch_bigt<128, 256, 2, 4, 3>(a, st);
+    case 43: return launch_bigt<128, 128, 2, 4, 4>(a, st);
 #ifdef YCX_EXPERIMENTAL_TILES  // retired experiments (tools/build_variant.sh NAME -DYCX_EXPERIMENTAL_TILES)
     case 27: return launch_p8<256, 256>(a, st);
     case 28: return launch_p8<128, 256>(a, st);

@@ -843,7 +843,8 @@ __device__ __forceinline__ void replace_slot16(unsigned short* sl, int rj) {
 
 template <int E>
 __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restrict__ ci, const Ptrs& P, char* smem, int (*s_lv)[5],
-                         int* s_ext, int* s_w, int* s_flag, const Thr& thr, float t_lo, float inv_t, int all_pairs) {
+                         int* s_ext, int* s_w, int* s_flag, const Thr& thr, float t_lo, float inv_t, int all_pairs,
+                         unsigned long long* s_prof) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int S = tk.S, off = tk.off;
   const int* bucket = P.bucket + off;
@@ -999,6 +1000,12 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
   __syncthreads();
   YCX_PROF_MARK(1)
   // (4) suppressors of every box (spatial order), kSlots highest-ranked kept (global slots)
+#ifdef YCX_NMS_PROFILE
+  const unsigned long long w_t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long w_vis = 0, w_mx = 0, w_ns = 0, w_over = 0;  // summed in registers: one atomic per wave
+  if (tid == 0) { s_prof[0] = 0; s_prof[1] = 0; }
+  __syncthreads();
+#endif
   for (int p = tid; p < S; p += kBigThreads) {
     const int r = lr[p];
     const f32x4 b = lbox[p];
@@ -1040,14 +1047,39 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
     });
     P.nsup[off + p] = ns;
 #ifdef YCX_NMS_PROFILE
-    if (ns > kFSlots) atomicAdd(&g_nms_prof[6], 1ull);
-    atomicAdd(&g_nms_prof[8], (unsigned long long)visits);
-    atomicAdd(&g_nms_prof[10], (unsigned long long)ns);
+    w_over += ns > kFSlots ? 1 : 0;
+    w_ns += ns;
     int mx = visits;
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
-    if (lane == 0) atomicAdd(&g_nms_prof[9], (unsigned long long)mx);
+    w_mx += mx;
+    w_vis += (unsigned long long)visits;
 #endif
   }
+#ifdef YCX_NMS_PROFILE
+  {  // per-wave search time and visits: the slowest wave bounds the phase
+    const unsigned long long d = __builtin_amdgcn_s_memtime() - w_t0;
+    unsigned long long v = w_vis, ns_ = w_ns, ov = w_over;
+    for (int o = 32; o > 0; o >>= 1) {
+      v += __shfl_xor(v, o);
+      ns_ += __shfl_xor(ns_, o);
+      ov += __shfl_xor(ov, o);
+    }
+    if (lane == 0) {
+      atomicAdd(&g_nms_prof[6], ov);
+      atomicAdd(&g_nms_prof[8], v);
+      atomicAdd(&g_nms_prof[9], w_mx);
+      atomicAdd(&g_nms_prof[10], ns_);
+      atomicAdd(&g_nms_prof[11], d);
+      atomicMax(&s_prof[0], d);
+      atomicMax(&s_prof[1], v);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      atomicAdd(&g_nms_prof[12], s_prof[0]);
+      atomicAdd(&g_nms_prof[13], s_prof[1]);
+    }
+  }
+#endif
   for (int r = tid; r < S; r += kBigThreads) st[r] = 0;
   // (5) suppressor lists into LDS (CSR over the dead box region), if they fit
   __syncthreads();  // every search read of lbox done: its region becomes the CSR
@@ -1155,6 +1187,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   __shared__ int s_ext[4];
   __shared__ int s_w[kBigThreads / 64];
   __shared__ int s_flag;
+  __shared__ unsigned long long s_prof[2];  // profile build: per-task wave maxima
   const int tid = threadIdx.x;
   const int rows = d.rows_total;
   const Layout L = layout(d.n, rows);
@@ -1180,7 +1213,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
       s_lv[tid][1] = s_lv[tid][2] = 0;  // +0.0f
       s_lv[tid][3] = s_lv[tid][4] = 0x7F800000;  // +inf
     }
-    big_fast<E>(tk, ci, P, smem, s_lv, s_ext, s_w, &s_flag, thr, t_lo, inv_t, all_pairs);
+    big_fast<E>(tk, ci, P, smem, s_lv, s_ext, s_w, &s_flag, thr, t_lo, inv_t, all_pairs, s_prof);
   }
 }
 

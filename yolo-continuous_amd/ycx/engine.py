@@ -937,10 +937,93 @@ class Engine:
     def run_static(self, events=None):
         self._ensure_static()
         ev = None
-        if events is not None:
+        ops, n_ops = self.ops, self.n_ops
+        if events is not None:  # per-op events: the plan's own op list
             ev = (ctypes.c_void_p * (self.n_ops + 1))(*[e.cuda_event for e in events])
-        L.check(L.lib.ycx_run_ops(self.ops, self.n_ops, L.stream_handle(self.device), ev), "ycx_run_ops")
+        else:
+            ops, n_ops = self._exec_ops()
+        L.check(L.lib.ycx_run_ops(ops, n_ops, L.stream_handle(self.device), ev), "ycx_run_ops")
         return self._result(self.fixed_outputs)
+
+    # ---- image-chunked prefix (experiment: keep the memory-bound high-resolution layers'
+    # working set in the 256 MiB Infinity Cache by running them k images at a time) ----
+    def _esize(self):
+        return {L.DT_BF16: 2, L.DT_F16: 2, L.DT_F32: 4, L.DT_FP8: 1}[self.dt]
+
+    def _chunk_op(self, op, i0, k):
+        """A copy of ``op`` restricted to images [i0, i0 + k): every operand is image-major,
+        so the restriction is n = k and a pointer offset per operand."""
+        o = L.Op()
+        ctypes.pointer(o)[0] = op
+        es = self._esize()
+
+        def shift(field, per_image):
+            v = getattr(o, field)
+            if v:
+                setattr(o, field, v + i0 * per_image)
+
+        if o.kind in (L.OP_CONV, L.OP_STEM, L.OP_STEM2):
+            d = o.d.pair[1] if o.kind == L.OP_STEM2 else o.d.conv
+            first = o.d.pair[0] if o.kind == L.OP_STEM2 else d
+            if o.kind == L.OP_CONV:
+                shift('in_', (4 if d.in_pool else 1) * d.h * d.w * d.in_c_stride * es)
+            else:  # fp32 NCHW image
+                shift('in_', first.cin * first.h * first.w * 4)
+            if d.out_layout == L.OUT_NCHW_F32:
+                shift('out', d.out_c_stride * d.ho * d.wo * 4)
+            else:
+                shift('out', (4 if d.out_layout == L.OUT_NHWC_UP2 else 1) * d.ho * d.wo * d.out_c_stride * es)
+            shift('residual', d.ho * d.wo * d.res_c_stride * es)
+            for dd in ((o.d.pair[0], o.d.pair[1]) if o.kind == L.OP_STEM2 else (o.d.conv,)):
+                dd.n = k
+        elif o.kind == L.OP_POOL:
+            d = o.d.pool
+            shift('in_', d.h * d.w * d.in_c_stride * es)
+            shift('out', d.ho * d.wo * d.out_c_stride * es)
+            d.n = k
+        elif o.kind == L.OP_COPY:
+            d = o.d.copy
+            shift('in_', d.h * d.w * d.in_c_stride * es)
+            if d.out_layout == L.OUT_NCHW_F32:
+                shift('out', d.out_c_stride * d.h * d.w * 4)
+            else:
+                shift('out', d.scale * d.scale * d.h * d.w * d.out_c_stride * es)
+            d.n = k
+        else:
+            raise ValueError("ycx: cannot chunk this op kind")
+        return o
+
+    @staticmethod
+    def _op_out_h(op):
+        if op.kind in (L.OP_CONV, L.OP_STEM, L.OP_HEAD):
+            return op.d.conv.ho
+        if op.kind == L.OP_STEM2:
+            return op.d.pair[1].ho
+        if op.kind == L.OP_POOL:
+            return op.d.pool.ho
+        return op.d.copy.h * op.d.copy.scale
+
+    def _exec_ops(self):
+        """The op array a forward runs: the plan, or with YCX_CHUNK='k:cut' its first ``cut``
+        ops run k images at a time (all of them for images 0..k-1, then k..2k-1, ...)."""
+        spec = os.environ.get('YCX_CHUNK')
+        n = self.shape[0]
+        if not spec:
+            return self.ops, self.n_ops
+        ks, cs = spec.split(':')
+        k = int(ks)
+        if cs.startswith('@'):  # '@H': every op up to the first whose output is below H rows
+            hmin, cut = int(cs[1:]), 0
+            while cut < self.n_ops and self._op_out_h(self.ops[cut]) >= hmin:
+                cut += 1
+        else:
+            cut = min(int(cs), self.n_ops)
+        if k <= 0 or k >= n or n % k or any(self.ops[i].kind == L.OP_HEAD for i in range(cut)):
+            return self.ops, self.n_ops
+        ops = [self._chunk_op(self.ops[i], i0, k) for i0 in range(0, n, k) for i in range(cut)]
+        ops += [self.ops[i] for i in range(cut, self.n_ops)]
+        self._chunked_ops = (L.Op * len(ops))(*ops)
+        return self._chunked_ops, len(ops)
 
     def capture(self):
         """Capture the static plan into a HIP graph (one launch per forward)."""
@@ -951,7 +1034,8 @@ class Engine:
             h = ctypes.c_void_p()
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
-            L.check(L.lib.ycx_graph_capture(self.ops, self.n_ops, s.cuda_stream, ctypes.byref(h)),
+            ops, n_ops = self._exec_ops()
+            L.check(L.lib.ycx_graph_capture(ops, n_ops, s.cuda_stream, ctypes.byref(h)),
                     "ycx_graph_capture")
             torch.cuda.current_stream(self.device).wait_stream(s)
             self.graph_exec = h.value
