@@ -478,11 +478,12 @@ def _random_pred(n, rows, nc, seed, scale=1.0, size_lo=-4.0, size_hi=0.0):
     return pred
 
 
+@pytest.mark.parametrize('rows', [6000, 24000])  # two classes each: LDS-resident fast path / nms_wide
 @pytest.mark.parametrize('thr', [0.0, 0.3, 0.65, 1.0])
-def test_nms_spatial_wide_sizes(device, thr):
+def test_nms_spatial_wide_sizes(device, thr, rows):
     """Large classes (spatial-grid path) with sizes spanning four octaves of
     ten, down to far below one grid cell: every level/window bound is used."""
-    _check_keep(_random_pred(2, 6000, 2, seed=11), 2, 0.0, thr)
+    _check_keep(_random_pred(2, rows, 2, seed=11), 2, 0.0, thr)
 
 
 def test_nms_spatial_pixel_coords_and_clusters(device):
@@ -496,8 +497,9 @@ def test_nms_spatial_pixel_coords_and_clusters(device):
     _check_keep(pred, 1, 0.0, 0.45)
 
 
-def test_nms_spatial_degenerate_and_identical(device):
-    pred = _random_pred(1, 3000, 1, seed=14, size_lo=-2.0, size_hi=-1.0)
+@pytest.mark.parametrize('rows', [3000, 12000])  # fast path / nms_wide
+def test_nms_spatial_degenerate_and_identical(device, rows):
+    pred = _random_pred(1, rows, 1, seed=14, size_lo=-2.0, size_hi=-1.0)
     pred[0, 0:200, 2] = 0.0                      # zero width
     pred[0, 200:400, 3] = -0.01                  # negative height (x2 < x1 after conversion)
     pred[0, 400:420, 0] = float('nan')           # NaN centre
@@ -521,3 +523,20 @@ def test_nms_spatial_long_chain(device):
     pred[0, :, 4] = 1.0 - i * 1e-4            # scores descend along the chain
     pred[0, :, 5] = 1.0
     _check_keep(pred, 1, 0.0, 0.3)
+
+
+def test_nms_big_class_score_ties(device):
+    """A large class (the LDS-resident fast path: radix rank sort) whose 4000 scores take
+    only 8 values: nearly every rank decision is the row tie-break of the stable
+    descending order (torchvision's sort), and the digits the keys share are skipped."""
+    pred = _random_pred(2, 4000, 1, seed=15, size_lo=-2.0, size_hi=-1.0)
+    g = torch.Generator().manual_seed(16)
+    pred[..., 4] = 0.5 + 0.0625 * torch.randint(0, 8, (2, 4000), generator=g).float()
+    pred[..., 5] = 1.0
+    _check_keep(pred, 1, 0.0, 0.3)
+    pred[..., 4] = 0.75  # one score for every box: the order is the row order alone
+    _check_keep(pred, 1, 0.0, 0.3)
+    wide = _random_pred(1, 20000, 1, seed=17, size_lo=-2.5, size_hi=-1.5)  # nms_wide's global radix sort
+    wide[..., 4] = 0.5 + 0.0625 * torch.randint(0, 8, (1, 20000), generator=g).float()
+    wide[..., 5] = 1.0
+    _check_keep(wide, 1, 0.0, 0.3)

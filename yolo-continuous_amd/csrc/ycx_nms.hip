@@ -742,6 +742,72 @@ constexpr int kFWild = fbase(kFLevels);  // boxes without a finite positive exte
 constexpr int kFCells = kFWild + 1;
 constexpr int kFCellBytes = ((kFCells + 1) / 2 * 4 + 255) & ~255;  // u16 end positions, packed in u32 words
 
+// Stable LSD radix sort of the S real keys held blocked in registers (element e = tid * E + i;
+// e >= S holds no key) by bits [lo, 64), 4-bit digits, digits that no two keys differ in
+// skipped. One pass: each thread's per-digit counts (nibbles of one u64, E <= 8 < 16) go to
+// a digit-major table T[16][kBigThreads] (u16), an exclusive scan of T in that order gives
+// every (digit, thread) its first output slot, the keys are scattered to dst in LDS and read
+// back blocked. Stable because a thread's elements keep their order inside a digit and
+// threads are ordered inside each digit, i.e. the (tid, i) order of the input is preserved.
+// The whole order is the 64-bit key order restricted to bits [lo, 64): with lo = 13 the fast
+// path's (score desc, row asc) order (the low 13 bits only name the element).
+template <int E>
+__device__ void radix_sort_regs(unsigned long long (&key)[E], int S, int lo, unsigned long long* dst,
+                                unsigned short* T, int* s_w, unsigned long long* s_msk) {
+  static_assert(E <= 8, "nibble counters");
+  const int tid = threadIdx.x, lane = tid & 63;
+  unsigned long long a = ~0ull, o = 0ull;
+#pragma unroll
+  for (int i = 0; i < E; ++i)
+    if (tid * E + i < S) { a &= key[i]; o |= key[i]; }
+#pragma unroll
+  for (int sh = 32; sh > 0; sh >>= 1) {
+    a &= __shfl_xor(a, sh);
+    o |= __shfl_xor(o, sh);
+  }
+  if (tid == 0) { s_msk[0] = ~0ull; s_msk[1] = 0ull; }
+  __syncthreads();
+  if (lane == 0) {
+    atomicAnd(&s_msk[0], a);
+    atomicOr(&s_msk[1], o);
+  }
+  __syncthreads();
+  const unsigned long long diff = s_msk[0] ^ s_msk[1];
+  for (int sh = lo; sh < 64; sh += 4) {
+    if (((diff >> sh) & 0xF) == 0) continue;  // uniform: every key has the same digit here
+    unsigned long long cnt = 0;
+#pragma unroll
+    for (int i = 0; i < E; ++i)
+      if (tid * E + i < S) cnt += 1ull << (4 * ((key[i] >> sh) & 0xF));
+#pragma unroll
+    for (int d = 0; d < 16; ++d) T[d * kBigThreads + tid] = (unsigned short)((cnt >> (4 * d)) & 0xF);
+    __syncthreads();
+    {  // exclusive scan of T in (digit, thread) order: thread t owns entries 16 t .. 16 t + 15
+      int v[16], sum = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) { v[q] = T[16 * tid + q]; sum += v[q]; }
+      int total;
+      int run = block_exclusive(sum, s_w, &total);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) { T[16 * tid + q] = (unsigned short)run; run += v[q]; }
+    }
+    __syncthreads();
+    unsigned long long seen = 0;  // this thread's elements placed so far, per digit (nibbles)
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      if (tid * E + i >= S) continue;
+      const int d = (int)((key[i] >> sh) & 0xF);
+      dst[T[d * kBigThreads + tid] + (int)((seen >> (4 * d)) & 0xF)] = key[i];
+      seen += 1ull << (4 * d);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < E; ++i)
+      if (tid * E + i < S) key[i] = dst[tid * E + i];
+    __syncthreads();  // every read of dst and T done before the next pass rewrites them
+  }
+}
+
 // LDS bytes of the fast path for a class of S boxes (cells, boxes, u16 ranks, state)
 __host__ __device__ inline int fast_lds_bytes(int S) { return kFCellBytes + 16 * S + ((2 * S + 15) & ~15) + S; }
 
@@ -781,18 +847,18 @@ __device__ __forceinline__ float reach(float wi, float nw, float mw, float t) {
 }
 
 __device__ __forceinline__ int u16_at(const unsigned* w, int k) { return (int)((w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu); }
-__device__ __forceinline__ int fcell_start(const unsigned* w, int k) { return k ? u16_at(w, k - 1) : 0; }
 
 // Position ranges [q0, q1) of the spatial order that can hold a suppressor of the
-// box of geometry g (as for_ranges, with the fast path's grid and tight window).
-template <class F>
-__device__ __forceinline__ void f_ranges(const unsigned* cells, const int (*lv)[5], const FGeo& g, int S,
-                                         float t_lo, float inv_t, F&& run) {
+// box of geometry g (as for_ranges, with the fine grid and the tight window);
+// cend(k) = end position of cell k (u16 words in the fast path, u32 in the wide one).
+template <class CE, class F>
+__device__ __forceinline__ void f_ranges(CE&& cend, const int (*lv)[5], const FGeo& g, int S, float t_lo,
+                                         float inv_t, F&& run) {
   if (g.level < 0) {
     run(0, S);
     return;
   }
-  run(fcell_start(cells, kFWild), u16_at(cells, kFWild));
+  run(cend(kFWild - 1), cend(kFWild));
   constexpr float kSlack = 1e-6f, kEps = 1e-5f;
   for (int L = 0; L < kFLevels; ++L) {
     if (lv[L][0] == 0) continue;
@@ -807,7 +873,7 @@ __device__ __forceinline__ void f_ranges(const unsigned* cells, const int (*lv)[
     const int iy0 = clamp_cell((g.cy - ry) * Gf, G), iy1 = clamp_cell((g.cy + ry) * Gf, G);
     for (int iy = iy0; iy <= iy1; ++iy) {  // cells ix0..ix1 of a grid row are contiguous positions
       const int k0 = base + iy * G + ix0, k1 = base + iy * G + ix1;
-      run(fcell_start(cells, k0), u16_at(cells, k1));
+      run(k0 ? cend(k0 - 1) : 0, cend(k1));
     }
   }
 }
@@ -844,7 +910,7 @@ __device__ __forceinline__ void replace_slot16(unsigned short* sl, int rj) {
 template <int E>
 __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restrict__ ci, const Ptrs& P, char* smem, int (*s_lv)[5],
                          int* s_ext, int* s_w, int* s_flag, const Thr& thr, float t_lo, float inv_t, int all_pairs,
-                         unsigned long long* s_prof) {
+                         unsigned long long* s_prof, unsigned long long* s_msk) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int S = tk.S, off = tk.off;
   const int* bucket = P.bucket + off;
@@ -869,7 +935,11 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
   // (2) rank sort in registers (exchange through LDS), then every element learns its rank
   unsigned long long* xch = reinterpret_cast<unsigned long long*>(smem);
   unsigned short* rank_of = reinterpret_cast<unsigned short*>(smem + 8 * kFastMax);
+#ifdef YCX_NMS_BITONIC  // development A/B: the bitonic sort of the general path
   sort_regs<E>(key, xch, E * kBigThreads);
+#else
+  radix_sort_regs<E>(key, S, 13, xch, reinterpret_cast<unsigned short*>(smem + 10 * kFastMax), s_w, s_msk);
+#endif
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < E; ++i)
@@ -1027,7 +1097,7 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
         ++ns;
       }
     };
-    f_ranges(cells, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
+    f_ranges([&](int k) { return u16_at(cells, k); }, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
 #ifdef YCX_NMS_PROFILE
       visits += q1 - q0;
 #endif
@@ -1132,7 +1202,7 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
         const float a = box_area(b);
         const FGeo g = fgeometry(b, X0, Y0, inv, all_pairs);
         bool stop = false;
-        f_ranges(cells, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
+        f_ranges([&](int k) { return u16_at(cells, k); }, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
           for (int q = q0; q < q1 && !stop; ++q) {
             const int rj = P.srank[off + q];
             if (rj >= r) continue;
@@ -1188,6 +1258,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   __shared__ int s_w[kBigThreads / 64];
   __shared__ int s_flag;
   __shared__ unsigned long long s_prof[2];  // profile build: per-task wave maxima
+  __shared__ unsigned long long s_msk[2];   // radix sort: AND / OR of the keys
   const int tid = threadIdx.x;
   const int rows = d.rows_total;
   const Layout L = layout(d.n, rows);
@@ -1213,7 +1284,342 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
       s_lv[tid][1] = s_lv[tid][2] = 0;  // +0.0f
       s_lv[tid][3] = s_lv[tid][4] = 0x7F800000;  // +inf
     }
-    big_fast<E>(tk, ci, P, smem, s_lv, s_ext, s_w, &s_flag, thr, t_lo, inv_t, all_pairs, s_prof);
+    big_fast<E>(tk, ci, P, smem, s_lv, s_ext, s_w, &s_flag, thr, t_lo, inv_t, all_pairs, s_prof, s_msk);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// nms_wide: classes past the LDS-resident fast path (S > kFastMax or too big for LDS:
+// the 1280^2 C4 load has ~18k-box classes). The fast path's algorithm with global
+// arrays where LDS runs out: a stable LSD radix rank sort of the workspace keys
+// (replacing the general path's global bitonic, O(S log^2 S) passes over global
+// memory), one gather per box into a rank-ordered copy, the fine grid (u32 cells in
+// LDS) and the tight window, int suppressor slots with one-read replacement, and the
+// fixed point over an LDS state array when S fits.
+// ---------------------------------------------------------------------------
+template <class F>
+__device__ __forceinline__ void for_slots32(const int* sl, int c, F&& f) {
+  const int4* s4 = reinterpret_cast<const int4*>(sl);
+  for (int q = 0; q < (c + 3) / 4; ++q) {
+    const int4 x = s4[q];
+    const int w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+      if (4 * q + h < c) f(4 * q + h, w[h]);
+  }
+}
+
+__device__ __forceinline__ void replace_slot32(int* sl, int rj) {  // keep the kSlots smallest ranks
+  int km = 0, vm = -1;
+  for_slots32(sl, kSlots, [&](int k, int v) {
+    km = v > vm ? k : km;
+    vm = v > vm ? v : vm;
+  });
+  if (rj < vm) sl[km] = rj;
+}
+
+// Stable LSD radix sort (4-bit digits, digits every key shares skipped) of S 64-bit keys
+// in global memory, ping-ponging between a and b; returns the buffer holding the result.
+// Blocked layout: thread t owns elements [t E, t E + E), E = ceil(S / kBigThreads) <= 128,
+// so per-thread digit counts fit 8-bit counters (two u64); T = LDS u32 [16][kBigThreads].
+__device__ unsigned long long* radix_sort_global(unsigned long long* a, unsigned long long* b, int S,
+                                                 unsigned* T, int* s_w, unsigned long long* s_msk) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int E = (S + kBigThreads - 1) / kBigThreads;
+  const int e0 = min(S, tid * E), e1 = min(S, e0 + E);
+  unsigned long long an = ~0ull, orr = 0ull;
+  for (int e = e0; e < e1; ++e) {
+    const unsigned long long k = a[e];
+    an &= k;
+    orr |= k;
+  }
+#pragma unroll
+  for (int sh = 32; sh > 0; sh >>= 1) {
+    an &= __shfl_xor(an, sh);
+    orr |= __shfl_xor(orr, sh);
+  }
+  if (tid == 0) { s_msk[0] = ~0ull; s_msk[1] = 0ull; }
+  __syncthreads();
+  if (lane == 0) {
+    atomicAnd(&s_msk[0], an);
+    atomicOr(&s_msk[1], orr);
+  }
+  __syncthreads();
+  const unsigned long long diff = s_msk[0] ^ s_msk[1];
+  for (int sh = 0; sh < 64; sh += 4) {
+    if (((diff >> sh) & 0xF) == 0) continue;  // uniform
+    unsigned long long c_lo = 0, c_hi = 0;    // 8-bit counters: digits 0-7, 8-15
+    for (int e = e0; e < e1; ++e) {
+      const int d = (int)((a[e] >> sh) & 0xF);
+      if (d < 8) c_lo += 1ull << (8 * d); else c_hi += 1ull << (8 * (d - 8));
+    }
+#pragma unroll
+    for (int d = 0; d < 16; ++d)
+      T[d * kBigThreads + tid] = (unsigned)(((d < 8 ? c_lo : c_hi) >> (8 * (d & 7))) & 0xFF);
+    __syncthreads();
+    {
+      unsigned v[16];
+      int sum = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) { v[q] = T[16 * tid + q]; sum += (int)v[q]; }
+      int total;
+      unsigned run = (unsigned)block_exclusive(sum, s_w, &total);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) { T[16 * tid + q] = run; run += v[q]; }
+    }
+    __syncthreads();
+    unsigned long long s_lo = 0, s_hi = 0;  // this thread's elements placed per digit
+    for (int e = e0; e < e1; ++e) {
+      const unsigned long long k = a[e];
+      const int d = (int)((k >> sh) & 0xF);
+      const unsigned seen = (unsigned)(((d < 8 ? s_lo : s_hi) >> (8 * (d & 7))) & 0xFF);
+      b[T[d * kBigThreads + tid] + seen] = k;
+      if (d < 8) s_lo += 1ull << (8 * d); else s_hi += 1ull << (8 * (d - 8));
+    }
+    __syncthreads();  // b complete (and every read of a and T done) before the next pass
+    unsigned long long* t = a;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_wide(
+    ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws, Thr thr, float t_lo, float inv_t, int all_pairs) {
+  constexpr int kCellB = ((kFCells * 4) + 255) & ~255;  // u32 cell ends
+  static_assert(kBigLds >= 16 * kBigThreads * 4 && kBigLds >= kCellB + 1024, "wide path LDS");
+  __shared__ __attribute__((aligned(16))) char smem[kBigLds];
+  __shared__ int s_lv[kFLevels][5];
+  __shared__ int s_ext[4];
+  __shared__ int s_w[kBigThreads / 64];
+  __shared__ int s_flag;
+  __shared__ unsigned long long s_msk[2];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int rows = d.rows_total;
+  const Layout L = layout(d.n, rows);
+  const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
+  const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks);
+  const int ntasks = hdr->ntasks;
+  unsigned* cells = reinterpret_cast<unsigned*>(smem);
+  for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
+    const Task tk = tasks[t];
+    const int S = tk.S, off = tk.off;
+#ifndef YCX_NMS_NO_FAST
+    if (S <= kFastMax && fast_lds_bytes(S) <= kBigLds) continue;  // nms_fast's task (uniform)
+#endif
+    const Ptrs P = image_ptrs(ws, L, tk.img);
+    const ycx_cand* ci = cand + (size_t)tk.img * rows;
+    int* bucket = P.bucket + off;
+#ifdef YCX_NMS_PROFILE
+    unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
+    if (tid == 0) atomicAdd(&g_nms_prof[7], 1ull);
+#endif
+    if (tid == 0) {
+      s_ext[0] = s_ext[1] = 0x7FFFFFFF;
+      s_ext[2] = s_ext[3] = (int)0x80000000;
+    }
+    if (tid < kFLevels) {
+      s_lv[tid][0] = 0;
+      s_lv[tid][1] = s_lv[tid][2] = 0;
+      s_lv[tid][3] = s_lv[tid][4] = 0x7F800000;
+    }
+    // (1) keys (score desc, row asc) in the workspace, radix-sorted: rank r = position
+    unsigned long long* ka = P.keys + 2 * (size_t)off;
+    for (int e = tid; e < S; e += kBigThreads) ka[e] = make_key(ci[bucket[e]]);
+    __syncthreads();
+    const unsigned long long* sorted =
+        radix_sort_global(ka, ka + S, S, reinterpret_cast<unsigned*>(smem), s_w, s_msk);
+    for (int r = tid; r < S; r += kBigThreads) bucket[r] = (int)(unsigned)sorted[r];  // bucket in rank order
+    __syncthreads();
+    YCX_PROF_MARK(0)
+    // (2) boxes in rank order (the dead keys' region, 16 B per rank) and the class extent
+    f32x4* rbox = reinterpret_cast<f32x4*>(ka);
+    {
+      int mn0 = 0x7FFFFFFF, mn1 = 0x7FFFFFFF, mx2 = (int)0x80000000, mx3 = (int)0x80000000;
+      for (int r = tid; r < S; r += kBigThreads) {
+        const ycx_cand c = ci[bucket[r]];
+        rbox[r] = f32x4{c.x1, c.y1, c.x2, c.y2};
+        if (c.x2 > c.x1 && c.y2 > c.y1 && c.x1 > -INFINITY && c.y1 > -INFINITY && c.x2 < INFINITY && c.y2 < INFINITY) {
+          mn0 = min(mn0, f2o(c.x1));
+          mn1 = min(mn1, f2o(c.y1));
+          mx2 = max(mx2, f2o(c.x2));
+          mx3 = max(mx3, f2o(c.y2));
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        mn0 = min(mn0, __shfl_xor(mn0, o));
+        mn1 = min(mn1, __shfl_xor(mn1, o));
+        mx2 = max(mx2, __shfl_xor(mx2, o));
+        mx3 = max(mx3, __shfl_xor(mx3, o));
+      }
+      if (lane == 0) {
+        atomicMin(&s_ext[0], mn0);
+        atomicMin(&s_ext[1], mn1);
+        atomicMax(&s_ext[2], mx2);
+        atomicMax(&s_ext[3], mx3);
+      }
+    }
+    for (int k = tid; k < kFCells; k += kBigThreads) cells[k] = 0;
+    __syncthreads();
+    const float X0 = o2f(s_ext[0]), Y0 = o2f(s_ext[1]);
+    const float Ex = fmaxf(o2f(s_ext[2]) - X0, o2f(s_ext[3]) - Y0);
+    const float inv = (Ex > 0.0f && Ex < INFINITY) ? 1.0f / Ex : 0.0f;
+    // (3) spatial counting sort on the fine grid (uniform trip count: the level ballots)
+    for (int r0 = 0; r0 < S; r0 += kBigThreads) {
+      const int r = r0 + tid;
+      FGeo g;
+      g.level = -1;
+      if (r < S) {
+        g = fgeometry(rbox[r], X0, Y0, inv, all_pairs);
+        atomicAdd(&cells[g.cell], 1u);
+      }
+      for (int Lv = 0; Lv < kFLevels; ++Lv) {
+        const bool in = r < S && g.level == Lv;
+        const unsigned long long m = __ballot(in);
+        if (!m) continue;
+        int mxw = in ? __float_as_int(g.w) : 0, mxh = in ? __float_as_int(g.h) : 0;
+        int mnw = in ? __float_as_int(g.w) : 0x7F800000, mnh = in ? __float_as_int(g.h) : 0x7F800000;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          mxw = max(mxw, __shfl_xor(mxw, o));
+          mxh = max(mxh, __shfl_xor(mxh, o));
+          mnw = min(mnw, __shfl_xor(mnw, o));
+          mnh = min(mnh, __shfl_xor(mnh, o));
+        }
+        if (lane == 0) {
+          atomicAdd(&s_lv[Lv][0], __popcll(m));
+          atomicMax(&s_lv[Lv][1], mxw);
+          atomicMax(&s_lv[Lv][2], mxh);
+          atomicMin(&s_lv[Lv][3], mnw);
+          atomicMin(&s_lv[Lv][4], mnh);
+        }
+      }
+    }
+    __syncthreads();
+    {  // exclusive scan of the cell counts in place
+      constexpr int kPer = (kFCells + kBigThreads - 1) / kBigThreads;
+      const int c0 = tid * kPer, c1 = min(kFCells, c0 + kPer);
+      int sum = 0;
+      for (int k = c0; k < c1; ++k) sum += (int)cells[k];
+      int total;
+      int run = block_exclusive(sum, s_w, &total);
+      __syncthreads();
+      for (int k = c0; k < c1; ++k) {
+        const int v = (int)cells[k];
+        cells[k] = (unsigned)run;
+        run += v;
+      }
+    }
+    __syncthreads();
+    f32x4* sbox = P.sbox + off;
+    int* srank = P.srank + off;
+    for (int r = tid; r < S; r += kBigThreads) {
+      const f32x4 b = rbox[r];
+      const int q = (int)atomicAdd(&cells[fgeometry(b, X0, Y0, inv, all_pairs).cell], 1u);  // -> cell ends
+      sbox[q] = b;
+      srank[q] = r;
+    }
+    __syncthreads();
+    YCX_PROF_MARK(1)
+    auto cend = [&](int k) { return (int)cells[k]; };
+    // (4) suppressors (kSlots highest-ranked) of every box, spatial order
+    for (int p = tid; p < S; p += kBigThreads) {
+      const int r = srank[p];
+      const f32x4 b = sbox[p];
+      const float a = box_area(b);
+      const FGeo g = fgeometry(b, X0, Y0, inv, all_pairs);
+      int* sl = P.slots + (size_t)(off + p) * kSlots;
+      int ns = 0;
+      auto test = [&](int rj, const f32x4& o) {
+        const bool cnd = rj < r && (all_pairs || (o[0] < b[2] && o[2] > b[0] && o[1] < b[3] && o[3] > b[1]));
+        if (cnd && suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
+          if (ns < kSlots) sl[ns] = rj;
+          else replace_slot32(sl, rj);
+          ++ns;
+        }
+      };
+      f_ranges(cend, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
+        int q = q0;
+        for (; q + 4 <= q1; q += 4) {
+          int rj[4];
+          f32x4 o[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            rj[u] = srank[q + u];
+            o[u] = sbox[q + u];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) test(rj[u], o[u]);
+        }
+        for (; q < q1; ++q) test(srank[q], sbox[q]);
+      });
+      P.nsup[off + p] = ns;
+    }
+    // (5) fixed point: state by rank in LDS beside the cells when it fits
+    unsigned char* st = S <= kBigLds - kCellB ? reinterpret_cast<unsigned char*>(smem + kCellB) : P.state + off;
+    for (int r = tid; r < S; r += kBigThreads) st[r] = 0;
+    __syncthreads();
+    YCX_PROF_MARK(2)
+    for (int it = 0; it <= S; ++it) {  // every round decides at least one box
+      if (tid == 0) s_flag = 0;
+      __syncthreads();
+      int undecided = 0;
+      for (int p = tid; p < S; p += kBigThreads) {
+        const int r = srank[p];
+        if (st[r] != 0) continue;
+        const int ns = P.nsup[off + p];
+        int res = 0;  // 0: every suppressor removed, 1: some undecided, 2: one kept
+        for_slots32(P.slots + (size_t)(off + p) * kSlots, min(ns, kSlots), [&](int, int v) {
+          const unsigned char sj = st[v];
+          res = res == 2 ? 2 : (sj == 1 ? 2 : (sj == 0 ? 1 : res));
+        });
+        if (ns > kSlots && res == 0) {  // the cached ones are all removed: rescan
+          const f32x4 b = sbox[p];
+          const float a = box_area(b);
+          const FGeo g = fgeometry(b, X0, Y0, inv, all_pairs);
+          bool stop = false;
+          f_ranges(cend, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
+            for (int q = q0; q < q1 && !stop; ++q) {
+              const int rj = srank[q];
+              if (rj >= r) continue;
+              const unsigned char sj = st[rj];
+              if (sj == 2) continue;
+              const f32x4 o = sbox[q];
+              if (suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
+                if (sj == 1) { res = 2; stop = true; }
+                else res = 1;
+              }
+            }
+          });
+        }
+        if (res == 2) st[r] = 2;
+        else if (res == 0) st[r] = 1;
+        else undecided = 1;
+      }
+      if (undecided) s_flag = 1;
+      __syncthreads();
+      const int more = s_flag;
+      __syncthreads();
+#ifdef YCX_NMS_PROFILE
+      if (tid == 0) atomicAdd(&g_nms_prof[5], 1ull);
+#endif
+      if (!more) break;
+    }
+    YCX_PROF_MARK(3)
+    // (6) kept rows in rank order
+    int base = 0;
+    for (int r0 = 0; r0 < S; r0 += kBigThreads) {
+      const int r = r0 + tid;
+      const int k = (r < S && st[r] == 1) ? 1 : 0;
+      int total;
+      const int pos = block_exclusive(k, s_w, &total);
+      if (k) P.kept[off + base + pos] = bucket[r];
+      base += total;
+    }
+    if (tid == 0) P.kc[tk.cls] = base;
+    __syncthreads();
+    YCX_PROF_MARK(4)
   }
 }
 
@@ -1224,7 +1630,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   constexpr int kLdsCellBytes = ((kCells * 4) + 255) & ~255;
   // register sorts exchange through LDS when the keys fit (Pn <= kLdsBytes / 8), else the workspace
   static_assert(kLdsBytes >= 8 * kBigThreads * 8 && kLdsBytes >= ((kCells * 4 + 255) & ~255) + 1024, "LDS budget");
-  static_assert(kLdsBytes >= 10 * kFastMax, "fast path: sort exchange + rank table");
+  static_assert(kLdsBytes >= 10 * kFastMax + 32 * kBigThreads, "fast path: sort buffers + rank table");
   static_assert(kFSlots * 2 == kSlots * 4 && kFastMax <= 65536, "fast path: u16 slots in the general path's rows");
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
   __shared__ int s_lv[kLevels][5];
@@ -1482,7 +1888,11 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   hipLaunchKernelGGL(nms_fast<2>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
   hipLaunchKernelGGL(nms_fast<1>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
 #endif
+#ifdef YCX_NMS_OLD_BIG  // development A/B: the r02 general path for every class the fast path leaves
   hipLaunchKernelGGL(nms_big, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
+#else
+  hipLaunchKernelGGL(nms_wide, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
+#endif
   hipLaunchKernelGGL(nms_finish, dim3(d->n), dim3(kThreads), 0, st, *d, cand, ws, dets, keep_rows, keep_counts);
   return ycx_launch_status();
 }
