@@ -20,12 +20,12 @@ PHASES = ["sort", "spatial", "suppressors", "rounds", "compact"]
 
 
 def main():
-    args = bench.parse(["--cpu-seconds", "0"])
+    args = bench.parse(["--cpu-seconds", "0"] + os.environ.get("NMS_PROBE_ARGS", "").split())
     dev = torch.device("cuda:0")
     _, det, _, _, _ = bench.setup(args, dev, use_graph=False)
     det()
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 24)()
     prof = hasattr(L.lib, "ycx_nms_prof_read")  # False on the release library: post time only
     if not prof:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -58,6 +58,10 @@ def main():
           f"suppressor pairs/task {buf[10] / nt:.0f}")
     print(f"  search: mean wave {buf[11] / (16 * nt) / 1e3:.1f} kcycles, slowest wave {buf[12] / nt / 1e3:.1f} kcycles, "
           f"slowest wave's visits {buf[13] / nt:.0f} (mean {buf[8] / (16 * nt):.0f})")
+    wt = buf[16 + 7]
+    if wt:
+        print(f"  nms_wide: {wt // reps} tasks/step; " + "  ".join(
+            f"{n} {buf[16 + i] / wt / 1e3:.1f}" for i, n in enumerate(PHASES)) + f" kcycles/task; rounds/task {buf[21] / wt:.1f}")
     cnt = det.counts.cpu()
     print("candidates/img", cnt.float().mean().item())
     ws = det.ws.view(torch.int32).cpu()  # header (ntasks) then the task table {img, cls, off, S} at byte 256

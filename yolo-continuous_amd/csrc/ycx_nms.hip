@@ -67,14 +67,22 @@ constexpr int kCells = kGridCells + 1;
 #ifdef YCX_NMS_PROFILE
 // Development counters: shader cycles per nms_big phase, summed over tasks.
 __device__ unsigned long long g_nms_prof[16];
+__device__ unsigned long long g_nms_wprof[8];  // nms_wide: phases 0-4, [5] rounds, [7] tasks
 #define YCX_PROF_MARK(i)                                               \
   if (tid == 0) {                                                      \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime();      \
     atomicAdd(&g_nms_prof[i], now_ - t_prev_);                         \
     t_prev_ = now_;                                                    \
   }
+#define YCX_WPROF_MARK(i)                                              \
+  if (tid == 0) {                                                      \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();      \
+    atomicAdd(&g_nms_wprof[i], now_ - t_prev_);                        \
+    t_prev_ = now_;                                                    \
+  }
 #else
 #define YCX_PROF_MARK(i)
+#define YCX_WPROF_MARK(i)
 #endif
 
 struct Task {  // one large class
@@ -100,7 +108,7 @@ __host__ __device__ inline Layout layout(int n, int rows) {
   L.max_tasks = rows / (kRegMax + 1) + 1;
   L.hdr = 0;
   L.tasks = 256;
-  L.per_image_base = al(L.tasks + (size_t)n * L.max_tasks * sizeof(Task));
+  L.per_image_base = al(L.tasks + 2 * (size_t)n * L.max_tasks * sizeof(Task));  // fast list, then wide list
   size_t o = 0;
   // keys: a class at bucket offset `off` with S rows sorts at keys + 2*off; its
   // power-of-two span is < 2S and off + S <= rows, so 2*rows keys suffice.
@@ -119,8 +127,13 @@ __host__ __device__ inline Layout layout(int n, int rows) {
   return L;
 }
 
+// Whether a class of S > kRegMax candidates takes the LDS-resident fast path (nms_fast):
+// S <= 8192 (13-bit element ids, E <= 8 registers) and cells + 19 B per box fit the LDS.
+__host__ __device__ inline bool fast_task(int S);
+
 struct Hdr {
-  int ntasks;
+  int ntasks;  // the fast list: classes the LDS-resident path takes (nms_fast)
+  int nwide;   // the wide list (nms_wide / the r02 general path): the others
 };
 
 // Sort key within a class: score descending (inverted fp32 bits; scores are
@@ -418,7 +431,10 @@ __global__ void __launch_bounds__(kThreads) nms_prep(ycx_nms_desc d, const ycx_c
     const int S = __builtin_amdgcn_readfirstlane(s_cnt[c]);
     if (S == 0) continue;
     if (S > kRegMax) {
-      if (lane == 0) tasks[atomicAdd(&hdr->ntasks, 1)] = Task{img, c, s_off[c], S};
+      if (lane == 0) {
+        if (fast_task(S)) tasks[atomicAdd(&hdr->ntasks, 1)] = Task{img, c, s_off[c], S};
+        else tasks[(size_t)d.n * L.max_tasks + atomicAdd(&hdr->nwide, 1)] = Task{img, c, s_off[c], S};
+      }
       continue;
     }
     const int* bk = P.bucket + s_off[c];
@@ -810,6 +826,13 @@ __device__ void radix_sort_regs(unsigned long long (&key)[E], int S, int lo, uns
 
 // LDS bytes of the fast path for a class of S boxes (cells, boxes, u16 ranks, state)
 __host__ __device__ inline int fast_lds_bytes(int S) { return kFCellBytes + 16 * S + ((2 * S + 15) & ~15) + S; }
+__host__ __device__ inline bool fast_task(int S) {
+#ifdef YCX_NMS_NO_FAST
+  return false;
+#else
+  return S <= kFastMax && fast_lds_bytes(S) <= kBigLds;
+#endif
+}
 
 struct FGeo {
   float cx, cy, w, h;
@@ -1267,9 +1290,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   const int ntasks = hdr->ntasks;
   for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
     const Task tk = tasks[t];
-    const int S = tk.S;
-    if (!(S <= kFastMax && fast_lds_bytes(S) <= kBigLds)) continue;  // nms_big's task (uniform)
-    if (max(next_pow2(S), kBigThreads) / kBigThreads != E) continue;  // another width's launch
+
     const Ptrs P = image_ptrs(ws, L, tk.img);
     const ycx_cand* ci = cand + (size_t)tk.img * rows;
 #ifdef YCX_NMS_PROFILE
@@ -1328,10 +1349,15 @@ __device__ unsigned long long* radix_sort_global(unsigned long long* a, unsigned
   const int E = (S + kBigThreads - 1) / kBigThreads;
   const int e0 = min(S, tid * E), e1 = min(S, e0 + E);
   unsigned long long an = ~0ull, orr = 0ull;
-  for (int e = e0; e < e1; ++e) {
-    const unsigned long long k = a[e];
-    an &= k;
-    orr |= k;
+  for (int e = e0; e < e1; e += 8) {  // eight loads in flight per thread
+    unsigned long long k[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) k[u] = e + u < e1 ? a[e + u] : a[e];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      an &= k[u];
+      orr |= k[u];
+    }
   }
 #pragma unroll
   for (int sh = 32; sh > 0; sh >>= 1) {
@@ -1349,9 +1375,16 @@ __device__ unsigned long long* radix_sort_global(unsigned long long* a, unsigned
   for (int sh = 0; sh < 64; sh += 4) {
     if (((diff >> sh) & 0xF) == 0) continue;  // uniform
     unsigned long long c_lo = 0, c_hi = 0;    // 8-bit counters: digits 0-7, 8-15
-    for (int e = e0; e < e1; ++e) {
-      const int d = (int)((a[e] >> sh) & 0xF);
-      if (d < 8) c_lo += 1ull << (8 * d); else c_hi += 1ull << (8 * (d - 8));
+    for (int e = e0; e < e1; e += 8) {
+      unsigned long long k[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) k[u] = e + u < e1 ? a[e + u] : 0ull;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (e + u >= e1) break;
+        const int d = (int)((k[u] >> sh) & 0xF);
+        if (d < 8) c_lo += 1ull << (8 * d); else c_hi += 1ull << (8 * (d - 8));
+      }
     }
 #pragma unroll
     for (int d = 0; d < 16; ++d)
@@ -1369,12 +1402,18 @@ __device__ unsigned long long* radix_sort_global(unsigned long long* a, unsigned
     }
     __syncthreads();
     unsigned long long s_lo = 0, s_hi = 0;  // this thread's elements placed per digit
-    for (int e = e0; e < e1; ++e) {
-      const unsigned long long k = a[e];
-      const int d = (int)((k >> sh) & 0xF);
-      const unsigned seen = (unsigned)(((d < 8 ? s_lo : s_hi) >> (8 * (d & 7))) & 0xFF);
-      b[T[d * kBigThreads + tid] + seen] = k;
-      if (d < 8) s_lo += 1ull << (8 * d); else s_hi += 1ull << (8 * (d - 8));
+    for (int e = e0; e < e1; e += 8) {
+      unsigned long long k[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) k[u] = e + u < e1 ? a[e + u] : 0ull;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (e + u >= e1) break;
+        const int d = (int)((k[u] >> sh) & 0xF);
+        const unsigned seen = (unsigned)(((d < 8 ? s_lo : s_hi) >> (8 * (d & 7))) & 0xFF);
+        b[T[d * kBigThreads + tid] + seen] = k[u];
+        if (d < 8) s_lo += 1ull << (8 * d); else s_hi += 1ull << (8 * (d - 8));
+      }
     }
     __syncthreads();  // b complete (and every read of a and T done) before the next pass
     unsigned long long* t = a;
@@ -1399,20 +1438,18 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   const Layout L = layout(d.n, rows);
   const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
   const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks);
-  const int ntasks = hdr->ntasks;
+  const int ntasks = hdr->nwide;
+  tasks += (size_t)d.n * L.max_tasks;  // the wide list
   unsigned* cells = reinterpret_cast<unsigned*>(smem);
   for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
     const Task tk = tasks[t];
     const int S = tk.S, off = tk.off;
-#ifndef YCX_NMS_NO_FAST
-    if (S <= kFastMax && fast_lds_bytes(S) <= kBigLds) continue;  // nms_fast's task (uniform)
-#endif
     const Ptrs P = image_ptrs(ws, L, tk.img);
     const ycx_cand* ci = cand + (size_t)tk.img * rows;
     int* bucket = P.bucket + off;
 #ifdef YCX_NMS_PROFILE
     unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
-    if (tid == 0) atomicAdd(&g_nms_prof[7], 1ull);
+    if (tid == 0) atomicAdd(&g_nms_wprof[7], 1ull);
 #endif
     if (tid == 0) {
       s_ext[0] = s_ext[1] = 0x7FFFFFFF;
@@ -1425,19 +1462,26 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
     }
     // (1) keys (score desc, row asc) in the workspace, radix-sorted: rank r = position
     unsigned long long* ka = P.keys + 2 * (size_t)off;
-    for (int e = tid; e < S; e += kBigThreads) ka[e] = make_key(ci[bucket[e]]);
+    for (int e0 = tid; e0 < S; e0 += 4 * kBigThreads) {  // four gathers in flight per thread
+      int row[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) row[u] = e0 + u * kBigThreads < S ? bucket[e0 + u * kBigThreads] : -1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (row[u] >= 0) ka[e0 + u * kBigThreads] = make_key(ci[row[u]]);
+    }
     __syncthreads();
     const unsigned long long* sorted =
         radix_sort_global(ka, ka + S, S, reinterpret_cast<unsigned*>(smem), s_w, s_msk);
     for (int r = tid; r < S; r += kBigThreads) bucket[r] = (int)(unsigned)sorted[r];  // bucket in rank order
     __syncthreads();
-    YCX_PROF_MARK(0)
+    YCX_WPROF_MARK(0)
     // (2) boxes in rank order (the dead keys' region, 16 B per rank) and the class extent
     f32x4* rbox = reinterpret_cast<f32x4*>(ka);
     {
       int mn0 = 0x7FFFFFFF, mn1 = 0x7FFFFFFF, mx2 = (int)0x80000000, mx3 = (int)0x80000000;
       for (int r = tid; r < S; r += kBigThreads) {
-        const ycx_cand c = ci[bucket[r]];
+        const ycx_cand c = ci[bucket[r]];  // (the loop body is small: the compiler keeps several in flight)
         rbox[r] = f32x4{c.x1, c.y1, c.x2, c.y2};
         if (c.x2 > c.x1 && c.y2 > c.y1 && c.x1 > -INFINITY && c.y1 > -INFINITY && c.x2 < INFINITY && c.y2 < INFINITY) {
           mn0 = min(mn0, f2o(c.x1));
@@ -1521,7 +1565,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
       srank[q] = r;
     }
     __syncthreads();
-    YCX_PROF_MARK(1)
+    YCX_WPROF_MARK(1)
     auto cend = [&](int k) { return (int)cells[k]; };
     // (4) suppressors (kSlots highest-ranked) of every box, spatial order
     for (int p = tid; p < S; p += kBigThreads) {
@@ -1560,7 +1604,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
     unsigned char* st = S <= kBigLds - kCellB ? reinterpret_cast<unsigned char*>(smem + kCellB) : P.state + off;
     for (int r = tid; r < S; r += kBigThreads) st[r] = 0;
     __syncthreads();
-    YCX_PROF_MARK(2)
+    YCX_WPROF_MARK(2)
     for (int it = 0; it <= S; ++it) {  // every round decides at least one box
       if (tid == 0) s_flag = 0;
       __syncthreads();
@@ -1602,11 +1646,11 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
       const int more = s_flag;
       __syncthreads();
 #ifdef YCX_NMS_PROFILE
-      if (tid == 0) atomicAdd(&g_nms_prof[5], 1ull);
+      if (tid == 0) atomicAdd(&g_nms_wprof[5], 1ull);
 #endif
       if (!more) break;
     }
-    YCX_PROF_MARK(3)
+    YCX_WPROF_MARK(3)
     // (6) kept rows in rank order
     int base = 0;
     for (int r0 = 0; r0 < S; r0 += kBigThreads) {
@@ -1619,7 +1663,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
     }
     if (tid == 0) P.kc[tk.cls] = base;
     __syncthreads();
-    YCX_PROF_MARK(4)
+    YCX_WPROF_MARK(4)
   }
 }
 
@@ -1642,7 +1686,8 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   const Layout L = layout(d.n, rows);
   const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
   const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks);
-  const int ntasks = hdr->ntasks;
+  const int ntasks = hdr->nwide;
+  tasks += (size_t)d.n * L.max_tasks;  // the wide list
   int* cells = reinterpret_cast<int*>(smem);
   for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
     const Task tk = tasks[t];
@@ -1650,9 +1695,6 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
     const ycx_cand* ci = cand + (size_t)tk.img * rows;
     const int S = tk.S, off = tk.off;
     int* bucket = P.bucket + off;
-#ifndef YCX_NMS_NO_FAST
-    if (S <= kFastMax && fast_lds_bytes(S) <= kLdsBytes) continue;  // nms_fast's task (uniform)
-#endif
 #ifdef YCX_NMS_PROFILE
     unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
     if (tid == 0) atomicAdd(&g_nms_prof[7], 1ull);
@@ -1849,11 +1891,13 @@ Thr make_thr(double thr) {
 }  // namespace
 
 #ifdef YCX_NMS_PROFILE
-extern "C" int ycx_nms_prof_read(unsigned long long* out, int reset) {
+extern "C" int ycx_nms_prof_read(unsigned long long* out, int reset) {  // out[0..15] fast, [16..23] wide
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nms_prof), sizeof(g_nms_prof)) != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_nms_wprof), sizeof(g_nms_wprof)) != hipSuccess) return 1;
   if (reset) {
     unsigned long long z[16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_nms_prof), z, sizeof(z)) != hipSuccess) return 1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_nms_wprof), z, 8 * sizeof(unsigned long long)) != hipSuccess) return 1;
   }
   return 0;
 }
@@ -1883,10 +1927,9 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   const float inv_t = t_lo > 0.0f ? 1.0f / t_lo : INFINITY;
   hipLaunchKernelGGL(nms_prep, dim3(d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws, t);
 #ifndef YCX_NMS_NO_FAST
+  // one width for every fast class: the radix sort and the per-element loops skip the
+  // elements past S, so E = 8 costs a small class little, and one launch replaces four
   hipLaunchKernelGGL(nms_fast<8>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
-  hipLaunchKernelGGL(nms_fast<4>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
-  hipLaunchKernelGGL(nms_fast<2>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
-  hipLaunchKernelGGL(nms_fast<1>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
 #endif
 #ifdef YCX_NMS_OLD_BIG  // development A/B: the r02 general path for every class the fast path leaves
   hipLaunchKernelGGL(nms_big, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
