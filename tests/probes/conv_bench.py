@@ -53,7 +53,7 @@ def run(shape, tile, iters=20):
     p = k // 2
     ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
     cpad = 64 if cout <= 64 else -(-cout // 128) * 128
-    if tile in (11, 24, 25, 27, 29, 30, 40, 41):
+    if tile in (11, 24, 25, 27, 29, 30, 40, 41, 44, 45, 46, 47):
         cpad = -(-cout // 256) * 256
     if tile in (1, 4, 7, 9, 12, 14, 16, 20, 21, 26, 28, 31, 32, 42, 43) and cpad % 128:
         return None

@@ -32,6 +32,8 @@ def main():
         p = k // 2
         ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
         cpad = 64 if cout <= 64 else -(-cout // 128) * 128
+        if tile in (11, 24, 25, 40, 41, 44, 45, 46, 47):
+            cpad = -(-cout // 256) * 256
         x = torch.randn(n, h, w, cin, device=dev).to(torch.bfloat16)
         wt = (torch.randn(cpad, k * k * cin, device=dev) * 0.05).to(torch.bfloat16)
         b = torch.zeros(cpad, device=dev)

@@ -157,7 +157,7 @@ def test_conv3x3_ws64(device, n, hw, cout, act):
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize('tile', [40, 41, 42, 43])
+@pytest.mark.parametrize('tile', [40, 41, 42, 43, 44, 45, 46, 47])
 def test_conv_big_tile_residual_up2_slices(device, tile):
     """Tiles 40-43 (conv_bigt, 32-deep K stages): residual add, x2 upsample store, channel
     slices, a ragged pixel tail over several workgroups (M = 2 * 23 * 19 = 874)."""

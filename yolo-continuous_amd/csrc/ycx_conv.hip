@@ -984,7 +984,9 @@ __device__ __forceinline__ void vm_wait_stages(int younger) {  // younger stages
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
+// DPOS: where a step issues the DMA of stage t + NS - 1: 0 right after the barrier, 1 after the
+// fragment reads, 2 between the MFMA halves, 3 after the MFMAs (NS >= 3 keeps a step of lead).
+template <int BM, int BN, int WM, int WN, int NS, int DPOS = 0>
 __global__ void __launch_bounds__(WM * WN * 64) conv_bigt(ConvArgs a) {
   constexpr int NW = WM * WN, BK = 32, TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -994,6 +996,10 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bigt(ConvArgs a) {
   const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
   const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#ifdef YCX_GLDS_STAMP
+  unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long st_start = stamp_issue();
+#endif
   const int wm = wid / WN, wn = wid % WN;
   const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
   int ct, pt;
@@ -1048,12 +1054,20 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bigt(ConvArgs a) {
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nt) issue(s, s);
+#ifdef YCX_GLDS_STAMP
+  unsigned long long st_prev = stamp_issue();
+  stamp_sync();
+  st_sum[0] = st_prev - st_start;
+#endif
   for (int t = 0; t < nt; ++t) {
     // stage t is complete once at most its younger stages' DMAs remain
     vm_wait_stages<LPS>(min(NS - 2, nt - 1 - t));
+    STAMP(1);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);  // the slot of stage t - 1, read by all
+    STAMP(2);
+    if (DPOS == 0 && t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);  // the slot of stage t - 1, read by all
+    STAMP(3);
     const char* A = smem + (t % NS) * STAGE;
     const char* B = A + A_BYTES;
     eltx8 af[FM], bfr[FN];
@@ -1069,17 +1083,53 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bigt(ConvArgs a) {
       bfr[j] = *reinterpret_cast<const eltx8*>(B + r * 64 + ((c ^ swz<BK>(r)) << 4));
     }
     __builtin_amdgcn_sched_barrier(0);
+    if (DPOS == 1 && t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP(4);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = YCX_MFMA16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (DPOS == 2 && i == FM / 2 - 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+    if (DPOS == 3 && t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP(5);
+#ifdef YCX_GLDS_STAMP
+    stamp_sync();
+    st_sum[1] += st_t1 - st_prev;
+    st_sum[2] += st_t2 - st_t1;
+    st_sum[3] += st_t3 - st_t2;
+    st_sum[4] += st_t4 - st_t3;
+    st_sum[5] += st_t5 - st_t4;
+    st_prev = st_t5;
+#endif
   }
   f32x4 bpre[FM];
   bias8_prefetch<FM>(a, co0 + wm * TM, lane, bpre);
   epilogue_regs8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane, bpre);
+#ifdef YCX_GLDS_STAMP
+  {
+    const unsigned long long e = stamp_issue();
+    stamp_sync();
+    st_sum[6] = e - st_prev;
+    st_sum[7] = e - st_start;
+  }
+  if (lane < 8) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v = lane == b ? st_sum[b] : v;
+    atomicAdd(&g_glds_stamp[(wid & 15) * 8 + lane], v);
+  }
+  if (tid == 0) atomicAdd(&g_glds_stamp[128], 1ull);
+#endif
 }
 
 // -------------------------------------------------------------------------
@@ -2933,6 +2983,10 @@ const TileInfo kTiles[] = {
     {256, 128, 32, "big_co256_px128_k32_s3"},
     {128, 256, 32, "big_co128_px256_k32_s3"},
     {128, 128, 32, "big_co128_px128_k32_s4"},
+    {256, 128, 32, "big_co256_px128_k32_s3_dma_after_reads"},
+    {256, 128, 32, "big_co256_px128_k32_s3_dma_mid_mfma"},
+    {256, 128, 32, "big_co256_px128_k32_s3_dma_after_mfma"},
+    {256, 256, 32, "big_co256_px256_k32_s4_dma_after_mfma"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -3010,14 +3064,14 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
 }
 
 // tiles 40-43: conv_bigt (32-deep K stages, NS - 1 in flight)
-template <int BM, int BN, int WM, int WN, int NS>
+template <int BM, int BN, int WM, int WN, int NS, int DPOS = 0>
 ycx_status launch_bigt(ConvArgs a, hipStream_t st) {
   if (a.Cin % 32 || a.Cout_pad % BM || a.out_layout == YCX_OUT_NCHW_F32 || a.pool) return YCX_ERR_UNSUPPORTED;
   a.nsteps = a.KH * a.KW * (a.Cin / 32);
   a.n_ct = a.Cout_pad / BM;
   a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
   a.gc = glds_gc(a);
-  hipLaunchKernelGGL((conv_bigt<BM, BN, WM, WN, NS>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
+  hipLaunchKernelGGL((conv_bigt<BM, BN, WM, WN, NS, DPOS>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
   return ycx_launch_status();
 }
 
@@ -3366,6 +3420,10 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x,
     case 41: return launch_bigt<256, 128, 4, 2, 3>(a, st);
     case 42: return launch_bigt<128, 256, 2, 4, 3>(a, st);
     case 43: return launch_bigt<128, 128, 2, 4, 4>(a, st);
+    case 44: return launch_bigt<256, 128, 4, 2, 3, 1>(a, st);  // tile 41 with the DMA issue moved (DPOS)
+    case 45: return launch_bigt<256, 128, 4, 2, 3, 2>(a, st);
+    case 46: return launch_bigt<256, 128, 4, 2, 3, 3>(a, st);
+    case 47: return launch_bigt<256, 256, 4, 4, 4, 3>(a, st);  // tile 40 likewise
 #ifdef YCX_EXPERIMENTAL_TILES  // retired experiments (tools/build_variant.sh NAME -DYCX_EXPERIMENTAL_TILES)
     case 27: return launch_p8<256, 256>(a, st);
     case 28: return launch_p8<128, 256>(a, st);

@@ -90,10 +90,15 @@ struct Task {  // one large class
 };
 
 struct Layout {
-  size_t hdr, tasks, per_image_base;  // header + task table (batch), then per image:
+  size_t hdr, tasks, wframes, wcells, per_image_base;  // header + task tables + wide-class index (batch), then per image:
   size_t keys, bucket, kept, sbox, srank, nsup, slots, state, cnt, offs, kc, per_image;
-  int max_tasks;
+  int max_tasks, max_wide;  // big classes per image; wide classes per image
 };
+
+__host__ __device__ inline int wide_min_s();  // the smallest class the wide path can get
+__host__ __device__ inline size_t wide_cells_bytes();
+struct WFrame;  // per wide class: extent normalisation, level stats (nms_wide_a -> _s, _b)
+__host__ __device__ inline size_t wframe_bytes();
 
 __host__ __device__ inline int next_pow2(int v) {
   int p = 1;
@@ -108,7 +113,10 @@ __host__ __device__ inline Layout layout(int n, int rows) {
   L.max_tasks = rows / (kRegMax + 1) + 1;
   L.hdr = 0;
   L.tasks = 256;
-  L.per_image_base = al(L.tasks + 2 * (size_t)n * L.max_tasks * sizeof(Task));  // fast list, then wide list
+  L.max_wide = rows / wide_min_s() + 1;
+  L.wframes = al(L.tasks + 2 * (size_t)n * L.max_tasks * sizeof(Task));  // fast list, then wide list
+  L.wcells = al(L.wframes + (size_t)n * L.max_wide * wframe_bytes());
+  L.per_image_base = al(L.wcells + (size_t)n * L.max_wide * wide_cells_bytes());
   size_t o = 0;
   // keys: a class at bucket offset `off` with S rows sorts at keys + 2*off; its
   // power-of-two span is < 2S and off + S <= rows, so 2*rows keys suffice.
@@ -826,6 +834,20 @@ __device__ void radix_sort_regs(unsigned long long (&key)[E], int S, int lo, uns
 
 // LDS bytes of the fast path for a class of S boxes (cells, boxes, u16 ranks, state)
 __host__ __device__ inline int fast_lds_bytes(int S) { return kFCellBytes + 16 * S + ((2 * S + 15) & ~15) + S; }
+__host__ __device__ inline int wide_min_s() {
+#ifdef YCX_NMS_NO_FAST
+  return kRegMax + 1;
+#else
+  return min(kFastMax + 1, (kBigLds - kFCellBytes - 32) / 19 + 1);  // fast_task() fails from here on
+#endif
+}
+__host__ __device__ inline size_t wide_cells_bytes() { return ((size_t)kFCells * 4 + 255) & ~(size_t)255; }
+struct WFrame {
+  float X0, Y0, inv;
+  int img, cls, off, S, slot;
+  int lv[kFLevels][5];
+};
+__host__ __device__ inline size_t wframe_bytes() { return (sizeof(WFrame) + 15) & ~(size_t)15; }
 __host__ __device__ inline bool fast_task(int S) {
 #ifdef YCX_NMS_NO_FAST
   return false;
@@ -1341,22 +1363,35 @@ __device__ __forceinline__ void replace_slot32(int* sl, int rj) {  // keep the k
 
 // Stable LSD radix sort (4-bit digits, digits every key shares skipped) of S 64-bit keys
 // in global memory, ping-ponging between a and b; returns the buffer holding the result.
-// Blocked layout: thread t owns elements [t E, t E + E), E = ceil(S / kBigThreads) <= 128,
-// so per-thread digit counts fit 8-bit counters (two u64); T = LDS u32 [16][kBigThreads].
+// Striped layout (coalesced): element p = i * kBigThreads + tid, i < E = ceil(S / kBigThreads)
+// <= 128. A pass counts, per (digit, i, wave), the wave's elements of slot i with that digit
+// (the lanes with equal digits found by four ballots), scans the counts in (digit, i, wave)
+// order -- the input order within each digit -- and scatters every key to its count's
+// offset plus its rank among the equal-digit lanes below it: stable.
+// C = LDS u32 [16][E][16] (<= 128 KiB).
+__device__ __forceinline__ unsigned long long same_digit_lanes(int dg) {
+  unsigned long long m = ~0ull;
+#pragma unroll
+  for (int bit = 0; bit < 4; ++bit) {
+    const unsigned long long bl = __ballot((dg >> bit) & 1);
+    m &= ((dg >> bit) & 1) ? bl : ~bl;
+  }
+  return m;
+}
+
 __device__ unsigned long long* radix_sort_global(unsigned long long* a, unsigned long long* b, int S,
-                                                 unsigned* T, int* s_w, unsigned long long* s_msk) {
-  const int tid = threadIdx.x, lane = tid & 63;
+                                                 unsigned* C, int* s_w, unsigned long long* s_msk) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int NW = kBigThreads / 64;
   const int E = (S + kBigThreads - 1) / kBigThreads;
-  const int e0 = min(S, tid * E), e1 = min(S, e0 + E);
+  const unsigned long long lt = (1ull << lane) - 1ull;  // lanes below this one
   unsigned long long an = ~0ull, orr = 0ull;
-  for (int e = e0; e < e1; e += 8) {  // eight loads in flight per thread
-    unsigned long long k[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) k[u] = e + u < e1 ? a[e + u] : a[e];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      an &= k[u];
-      orr |= k[u];
+  for (int i = 0; i < E; ++i) {
+    const int p = i * kBigThreads + tid;
+    if (p < S) {
+      const unsigned long long k = a[p];
+      an &= k;
+      orr |= k;
     }
   }
 #pragma unroll
@@ -1372,50 +1407,41 @@ __device__ unsigned long long* radix_sort_global(unsigned long long* a, unsigned
   }
   __syncthreads();
   const unsigned long long diff = s_msk[0] ^ s_msk[1];
+  const int nC = 16 * E * NW;
   for (int sh = 0; sh < 64; sh += 4) {
     if (((diff >> sh) & 0xF) == 0) continue;  // uniform
-    unsigned long long c_lo = 0, c_hi = 0;    // 8-bit counters: digits 0-7, 8-15
-    for (int e = e0; e < e1; e += 8) {
-      unsigned long long k[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) k[u] = e + u < e1 ? a[e + u] : 0ull;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (e + u >= e1) break;
-        const int d = (int)((k[u] >> sh) & 0xF);
-        if (d < 8) c_lo += 1ull << (8 * d); else c_hi += 1ull << (8 * (d - 8));
-      }
-    }
-#pragma unroll
-    for (int d = 0; d < 16; ++d)
-      T[d * kBigThreads + tid] = (unsigned)(((d < 8 ? c_lo : c_hi) >> (8 * (d & 7))) & 0xFF);
+    for (int c = tid; c < nC; c += kBigThreads) C[c] = 0;
     __syncthreads();
-    {
-      unsigned v[16];
+    for (int i = 0; i < E; ++i) {  // uniform trip count: the ballots need every lane
+      const int p = i * kBigThreads + tid;
+      const bool ok = p < S;
+      const int dg = ok ? (int)((a[p] >> sh) & 0xF) : 16;  // 16: past the end (matches no digit)
+      const unsigned long long m = same_digit_lanes(dg & 15) & __ballot(ok);
+      if (ok && (m & lt) == 0) C[(dg * E + i) * NW + wid] = (unsigned)__popcll(m);  // the group's first lane
+    }
+    __syncthreads();
+    {  // exclusive scan of C in (digit, i, wave) order: thread t owns a contiguous run
+      const int per = (nC + kBigThreads - 1) / kBigThreads, c0 = min(nC, tid * per), c1 = min(nC, c0 + per);
       int sum = 0;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) { v[q] = T[16 * tid + q]; sum += (int)v[q]; }
+      for (int c = c0; c < c1; ++c) sum += (int)C[c];
       int total;
       unsigned run = (unsigned)block_exclusive(sum, s_w, &total);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) { T[16 * tid + q] = run; run += v[q]; }
-    }
-    __syncthreads();
-    unsigned long long s_lo = 0, s_hi = 0;  // this thread's elements placed per digit
-    for (int e = e0; e < e1; e += 8) {
-      unsigned long long k[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) k[u] = e + u < e1 ? a[e + u] : 0ull;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (e + u >= e1) break;
-        const int d = (int)((k[u] >> sh) & 0xF);
-        const unsigned seen = (unsigned)(((d < 8 ? s_lo : s_hi) >> (8 * (d & 7))) & 0xFF);
-        b[T[d * kBigThreads + tid] + seen] = k[u];
-        if (d < 8) s_lo += 1ull << (8 * d); else s_hi += 1ull << (8 * (d - 8));
+      for (int c = c0; c < c1; ++c) {
+        const unsigned v = C[c];
+        C[c] = run;
+        run += v;
       }
     }
-    __syncthreads();  // b complete (and every read of a and T done) before the next pass
+    __syncthreads();
+    for (int i = 0; i < E; ++i) {
+      const int p = i * kBigThreads + tid;
+      const bool ok = p < S;
+      const unsigned long long k = ok ? a[p] : 0ull;
+      const int dg = ok ? (int)((k >> sh) & 0xF) : 16;
+      const unsigned long long m = same_digit_lanes(dg & 15) & __ballot(ok);
+      if (ok) b[C[(dg * E + i) * NW + wid] + __popcll(m & lt)] = k;
+    }
+    __syncthreads();  // b complete (and every read of a and C done) before the next pass
     unsigned long long* t = a;
     a = b;
     b = t;
@@ -1423,15 +1449,15 @@ __device__ unsigned long long* radix_sort_global(unsigned long long* a, unsigned
   return a;
 }
 
-__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_wide(
+__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_wide_a(
     ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws, Thr thr, float t_lo, float inv_t, int all_pairs) {
   constexpr int kCellB = ((kFCells * 4) + 255) & ~255;  // u32 cell ends
-  static_assert(kBigLds >= 16 * kBigThreads * 4 && kBigLds >= kCellB + 1024, "wide path LDS");
+  static_assert(kBigLds >= 16 * (kMaxRows / kBigThreads) * (kBigThreads / 64) * 4 && kBigLds >= kCellB + 1024,
+                "wide path LDS: radix counts, cells");
   __shared__ __attribute__((aligned(16))) char smem[kBigLds];
   __shared__ int s_lv[kFLevels][5];
   __shared__ int s_ext[4];
   __shared__ int s_w[kBigThreads / 64];
-  __shared__ int s_flag;
   __shared__ unsigned long long s_msk[2];
   const int tid = threadIdx.x, lane = tid & 63;
   const int rows = d.rows_total;
@@ -1565,14 +1591,69 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
       srank[q] = r;
     }
     __syncthreads();
+    // publish the class's spatial index for the search and resolve launches
+    WFrame* fr = reinterpret_cast<WFrame*>(ws + L.wframes + (size_t)t * wframe_bytes());
+    unsigned* gcells = reinterpret_cast<unsigned*>(ws + L.wcells + (size_t)t * wide_cells_bytes());
+    for (int k = tid; k < kFCells; k += kBigThreads) gcells[k] = cells[k];
+    if (tid == 0) {
+      fr->X0 = X0;
+      fr->Y0 = Y0;
+      fr->inv = inv;
+      fr->img = tk.img;
+      fr->cls = tk.cls;
+      fr->off = off;
+      fr->S = S;
+    }
+    if (tid < kFLevels * 5) fr->lv[tid / 5][tid % 5] = s_lv[tid / 5][tid % 5];
     YCX_WPROF_MARK(1)
+    __syncthreads();
+  }
+}
+
+constexpr int kWChunk = 2048;  // positions per nms_wide_s item
+
+// load a wide class's frame (level stats to LDS) and cell table (to LDS); returns the frame
+__device__ __forceinline__ WFrame load_wide(const char* ws, const Layout& L, int t, unsigned* cells, int (*s_lv)[5]) {
+  const WFrame* fr = reinterpret_cast<const WFrame*>(ws + L.wframes + (size_t)t * wframe_bytes());
+  const unsigned* gcells = reinterpret_cast<const unsigned*>(ws + L.wcells + (size_t)t * wide_cells_bytes());
+  for (int k = threadIdx.x; k < kFCells; k += kBigThreads) cells[k] = gcells[k];
+  if (threadIdx.x < kFLevels * 5) s_lv[threadIdx.x / 5][threadIdx.x % 5] = fr->lv[threadIdx.x / 5][threadIdx.x % 5];
+  const WFrame f = *fr;
+  __syncthreads();
+  return f;
+}
+
+// Suppressor search of the wide classes, split into items of kWChunk positions so a
+// class's search runs on many CUs (one workgroup per item, grid-strided).
+__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_wide_s(
+    ycx_nms_desc d, char* ws, Thr thr, float t_lo, float inv_t, int all_pairs) {
+  __shared__ __attribute__((aligned(16))) unsigned cells[kFCells];
+  __shared__ int s_lv[kFLevels][5];
+  const int tid = threadIdx.x;
+  const Layout L = layout(d.n, d.rows_total);
+  const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
+  const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks) + (size_t)d.n * L.max_tasks;
+  const int ntasks = hdr->nwide;
+  int nitems = 0;
+  for (int t = 0; t < ntasks; ++t) nitems += (tasks[t].S + kWChunk - 1) / kWChunk;
+  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+    int t = 0, c = item;  // the item's class and chunk (uniform scan of the short task list)
+    while (c >= (tasks[t].S + kWChunk - 1) / kWChunk) {
+      c -= (tasks[t].S + kWChunk - 1) / kWChunk;
+      ++t;
+    }
+    const WFrame f = load_wide(ws, L, t, cells, s_lv);
+    const Ptrs P = image_ptrs(ws, L, f.img);
+    const int S = f.S, off = f.off;
+    const f32x4* sbox = P.sbox + off;
+    const int* srank = P.srank + off;
     auto cend = [&](int k) { return (int)cells[k]; };
-    // (4) suppressors (kSlots highest-ranked) of every box, spatial order
-    for (int p = tid; p < S; p += kBigThreads) {
+    const int p1 = min(S, (c + 1) * kWChunk);
+    for (int p = c * kWChunk + tid; p < p1; p += kBigThreads) {
       const int r = srank[p];
       const f32x4 b = sbox[p];
       const float a = box_area(b);
-      const FGeo g = fgeometry(b, X0, Y0, inv, all_pairs);
+      const FGeo g = fgeometry(b, f.X0, f.Y0, f.inv, all_pairs);
       int* sl = P.slots + (size_t)(off + p) * kSlots;
       int ns = 0;
       auto test = [&](int rj, const f32x4& o) {
@@ -1600,6 +1681,37 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
       });
       P.nsup[off + p] = ns;
     }
+    __syncthreads();  // every read of this item's cells done before the next item loads its own
+  }
+}
+
+// Greedy fixed point and compaction of the wide classes (one workgroup per class).
+__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_wide_b(
+    ycx_nms_desc d, char* ws, Thr thr, float t_lo, float inv_t, int all_pairs) {
+  constexpr int kCellB = ((kFCells * 4) + 255) & ~255;  // u32 cell ends
+  __shared__ __attribute__((aligned(16))) char smem[kBigLds];
+  __shared__ int s_lv[kFLevels][5];
+  __shared__ int s_w[kBigThreads / 64];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x;
+  const Layout L = layout(d.n, d.rows_total);
+  const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
+  const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks) + (size_t)d.n * L.max_tasks;
+  const int ntasks = hdr->nwide;
+  unsigned* cells = reinterpret_cast<unsigned*>(smem);
+  for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
+    const Task tk = tasks[t];
+#ifdef YCX_NMS_PROFILE
+    unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
+#endif
+    const WFrame f = load_wide(ws, L, t, cells, s_lv);
+    const Ptrs P = image_ptrs(ws, L, tk.img);
+    const int S = tk.S, off = tk.off;
+    const int* bucket = P.bucket + off;
+    const float X0 = f.X0, Y0 = f.Y0, inv = f.inv;
+    const f32x4* sbox = P.sbox + off;
+    const int* srank = P.srank + off;
+    auto cend = [&](int k) { return (int)cells[k]; };
     // (5) fixed point: state by rank in LDS beside the cells when it fits
     unsigned char* st = S <= kBigLds - kCellB ? reinterpret_cast<unsigned char*>(smem + kCellB) : P.state + off;
     for (int r = tid; r < S; r += kBigThreads) st[r] = 0;
@@ -1934,7 +2046,9 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
 #ifdef YCX_NMS_OLD_BIG  // development A/B: the r02 general path for every class the fast path leaves
   hipLaunchKernelGGL(nms_big, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
 #else
-  hipLaunchKernelGGL(nms_wide, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
+  hipLaunchKernelGGL(nms_wide_a, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
+  hipLaunchKernelGGL(nms_wide_s, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
+  hipLaunchKernelGGL(nms_wide_b, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
 #endif
   hipLaunchKernelGGL(nms_finish, dim3(d->n), dim3(kThreads), 0, st, *d, cand, ws, dets, keep_rows, keep_counts);
   return ycx_launch_status();
