@@ -86,37 +86,58 @@ def test_predict_headless(device, tmp_path):
     assert all(isinstance(b, TargetBox) for b in boxes)
 
 
-def test_predict_vs_oracle_chain(device, tmp_path):
+@pytest.mark.parametrize('precision,size,hw', [('f32', 320, (287, 411)), ('fp16', 640, (512, 773))])
+def test_predict_vs_oracle_chain(device, tmp_path, precision, size, hw):
     """predict (detect.py:208-265) against the oracle chain on the same image: the
     letterbox restatement (oracle/ref_letterbox.py), the fp32 forward
     (oracle/ref_forward.py), decode_box + non_max_suppression + yolo_correct_boxes
     (oracle/ref_post.py), then detect.py:236-244's floor/clamp. f32 parity mode
     (1e-3): the same boxes in the same order, corners within one pixel (a
-    floor can cross an integer), scores within 1e-3, same labels."""
+    floor can cross an integer), scores within 1e-3, same labels. fp16 (the
+    default precision) at 640 on a 773x512 image, BASELINE C1's plumbing shape:
+    the same boxes in the same order but for threshold flips (<= 2 %), matched
+    boxes held to the same bars."""
     from oracle import ref_forward, ref_letterbox, ref_post
     from ycx.utils.helper_io import cvt_cfg
     from ycx.utils.synth import synthetic_state_dict
-    plan = dict(device=0, image_size=320, image_chan=3, labels=['raccoon'], model_cfg='yolov7-tiny',
+    plan = dict(device=0, image_size=size, image_chan=3, labels=['raccoon'], model_cfg='yolov7-tiny',
                 anchors=ANCHORS, anchors_mask=MASK)
     cfg = tmp_path / 'plan.yaml'
     cfg.write_text(yaml.safe_dump(plan))
-    img = np.random.default_rng(4).integers(0, 256, size=(287, 411, 3), dtype=np.uint8)
+    img = np.random.default_rng(4).integers(0, 256, size=hw + (3,), dtype=np.uint8)
     got = predict(str(cfg), image=img, weights='synthetic', device='cuda:0', conf_threshold=0.3,
-                  nms_threshold=0.3, precision='f32')
+                  nms_threshold=0.3, precision=precision)
     net_cfg = cvt_cfg('yolov7-tiny')
     from ycx.nets.yolo import Model
     sd = synthetic_state_dict(Model(net_cfg, ANCHORS, 1), seed=0)
-    x = torch.from_numpy(ref_letterbox.letterbox_tensor(img, (320, 320))).unsqueeze(0)
+    x = torch.from_numpy(ref_letterbox.letterbox_tensor(img, (size, size))).unsqueeze(0)
     heads = ref_forward.build(net_cfg, ANCHORS, 1, sd)(x)
     A = np.asarray(ANCHORS).reshape(-1, 2)
-    dec = torch.cat(ref_post.decode_box(heads, A, MASK, 1, (320, 320)), 1)
-    res = ref_post.non_max_suppression(dec, 1, (320, 320), np.array(img.shape[0:2]), True, 0.3, 0.3)[0]
-    assert res is not None and len(got) == len(res) > 0, (len(got), None if res is None else len(res))
-    for tb, row in zip(got, res):
+    dec = torch.cat(ref_post.decode_box(heads, A, MASK, 1, (size, size)), 1)
+    res = ref_post.non_max_suppression(dec, 1, (size, size), np.array(img.shape[0:2]), True, 0.3, 0.3)[0]
+    assert res is not None and len(res) > 0
+
+    def close(tb, row):
         y1, x1, y2, x2 = row[0], row[1], row[2], row[3]
         want = [max(0, int(np.floor(x1))), max(0, int(np.floor(y1))),
                 min(img.shape[1], int(np.floor(x2))), min(img.shape[0], int(np.floor(y2)))]
-        assert max(abs(a - b) for a, b in zip([tb.left, tb.top, tb.right, tb.bottom], want)) <= 1
-        assert abs(float(tb.score) - float(row[4] * row[5])) <= 1e-3
-        assert tb.label == 'raccoon' and tb.color == (255, 0, 0)
+        return (max(abs(a - b) for a, b in zip([tb.left, tb.top, tb.right, tb.bottom], want)) <= 1 and
+                abs(float(tb.score) - float(row[4] * row[5])) <= 1e-3)
+
+    assert all(tb.label == 'raccoon' and tb.color == (255, 0, 0) for tb in got)
+    if precision == 'f32':
+        assert len(got) == len(res), (len(got), len(res))
+        assert all(close(tb, row) for tb, row in zip(got, res))
+        return
+    # fp16: walk both lists in order; a box present in only one of them is a threshold flip
+    i = j = matched = 0
+    while i < len(got) and j < len(res):
+        if close(got[i], res[j]):
+            matched, i, j = matched + 1, i + 1, j + 1
+        elif j + 1 < len(res) and close(got[i], res[j + 1]):
+            j += 1
+        else:
+            i += 1
+    print(f"\nfp16 predict: {len(got)} boxes, oracle {len(res)}, matched in order {matched}")
+    assert matched >= 0.98 * max(len(got), len(res)), (matched, len(got), len(res))
 

@@ -484,7 +484,7 @@ class ConcurrentDetector:
             d.close()
 
 
-def prepare_model(plan, weights=None, device=None, precision='bf16'):
+def prepare_model(plan, weights=None, device=None, precision='fp16'):
     """detect.py:168-180: build the Model from the plan and load its weights.
     ``weights`` overrides plan.save_path (a state_dict or a path, loaded with
     weights_only=True); 'synthetic' loads the seeded recipe of ycx.utils.synth."""
@@ -508,7 +508,7 @@ def prepare_model(plan, weights=None, device=None, precision='bf16'):
 
 
 def predict(cfg_file, image_path=None, conf_threshold=0.3, nms_threshold=0.3, *, image=None, device=None,
-            weights=None, show=False, precision='bf16'):
+            weights=None, show=False, precision='fp16'):
     """detect.py:208-265, headless by default. ``image`` may be an HWC uint8 BGR
     array instead of a path. Returns (and prints) the reference's TargetBox
     records (utils/target_box.py): corners floored and clamped to the image as

@@ -141,17 +141,19 @@ class Model(nn.Module):
 
     forward(x: fp32 [N, C, H, W] on a ROCm device) -> the last layer's output:
     ``[P5, P4, P3]`` fp32 NCHW logits for a Detect head (nets/detect.py:38).
-    ``precision`` selects the kernel dtype: 'bf16' (default, MFMA bf16, fp32
-    accumulate), 'fp16' (IEEE half activations and weights on the f16 MFMA:
-    the bf16 kernels at the bf16 rate with an 11-bit significand, the mode that
-    holds north_star's 1e-3 on box / confidence tensors; activations must stay
-    inside the fp16 range, |a| < 65504), 'f32' (exact-fp32 MFMA) or 'fp8' (OCP
+    ``precision`` selects the kernel dtype: 'fp16' (default: IEEE half
+    activations and weights on the f16 MFMA, fp32 accumulate -- the bf16 kernels
+    at the bf16 rate with an 11-bit significand, the mode that holds north_star's
+    1e-3 of the reference's fp32 forward on box / confidence tensors; activations
+    must stay inside the fp16 range, |a| < 65504 -- a checkpoint that overflows
+    it takes 'bf16' or 'f32'), 'bf16' (MFMA bf16, the BASELINE C2 bench
+    configuration, ~1e-3), 'f32' (exact-fp32 MFMA) or 'fp8' (OCP
     e4m3 weights and activations on the block-scaled MFMA, fp32 accumulate; the
     activation scales come from ``calibrate_fp8``).
     """
 
     def __init__(self, model_cfg, anchors, num_classes, image_chan=3, weight_initial=WeightInitial.Random,
-                 precision='bf16'):
+                 precision='fp16'):
         super().__init__()
         self.traced = False
         self.weight_initial = weight_initial
