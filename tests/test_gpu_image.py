@@ -93,8 +93,9 @@ def test_predict_vs_oracle_chain(device, tmp_path, precision, size, hw):
     letterbox restatement (oracle/ref_letterbox.py), the fp32 forward
     (oracle/ref_forward.py), decode_box + non_max_suppression + yolo_correct_boxes
     (oracle/ref_post.py), then detect.py:236-244's floor/clamp. f32 parity mode
-    (1e-3): the same boxes in the same order, corners within one pixel (a
-    floor can cross an integer), scores within 1e-3, same labels. fp16 (the
+    (1e-3): the same boxes in the same order (boxes whose oracle scores are within
+    1e-5 may trade places), corners within one pixel (a floor can cross an integer),
+    scores within 1e-3, same labels. fp16 (the
     default precision) at 640 on a 773x512 image, BASELINE C1's plumbing shape (also
     run in f32, strictly): the seeded weights keep ~1.9k heavily overlapping boxes of
     the one class, so a score that moves by ~1e-4 can flip a greedy decision and the
@@ -130,7 +131,19 @@ def test_predict_vs_oracle_chain(device, tmp_path, precision, size, hw):
     assert all(tb.label == 'raccoon' and tb.color == (255, 0, 0) for tb in got)
     if precision == 'f32':
         assert len(got) == len(res), (len(got), len(res))
-        assert all(close(tb, row) for tb, row in zip(got, res))
+        # same boxes in the same order, except that boxes whose scores the oracle itself puts
+        # within 1e-5 of each other (far inside the 1e-3 forward tolerance) may trade places:
+        # measured r03 on MI355X, 3 adjacent swaps in 1934 rows, score gaps <= 2e-7
+        score = [float(r[4] * r[5]) for r in res]
+        used, bad = set(), []
+        for i, tb in enumerate(got):
+            js = [j for j in range(max(0, i - 4), min(len(res), i + 5))
+                  if j not in used and (j == i or abs(score[j] - score[i]) <= 1e-5) and close(tb, res[j])]
+            if not js:
+                bad.append((i, (tb.left, tb.top, tb.right, tb.bottom, float(tb.score)), score[i]))
+            else:
+                used.add(i if i in js else js[0])
+        assert not bad, (len(bad), bad[:4])
         return
     # fp16: scores move by ~1e-4, so equal-class boxes of near-equal score may swap places and a
     # box at a threshold may flip: match as multisets (each oracle box to an unused predicted box
