@@ -1,0 +1,11 @@
+# packed-fp32 activations (stem2 + glds epilogue): kernel/model parity, stem2 timing, bench A/B vs HEAD (libycx_base)
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out/r03
+cd $R
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r03/s22_tests.log 2>&1 || { grep -E "^E  |FAILED" gpurun_out/r03/s22_tests.log | head -10; exit 1; }
+tail -1 gpurun_out/r03/s22_tests.log
+for v in base hip; do echo -n "$v "; YCX_LIB=$R/yolo-continuous_amd/ycx/libycx_$v.so timeout -k 10 120 python tests/probes/stem2_bench.py fused 2>&1 | grep -v amdgpu.ids | tail -1; done
+for v in base hip base hip; do
+YCX_LIB=$R/yolo-continuous_amd/ycx/libycx_$v.so timeout -k 10 300 python bench.py --cpu-seconds 0 --image-in-steps 0 > gpurun_out/r03/b22.log 2>&1 || { tail -20 gpurun_out/r03/b22.log; exit 1; }
+echo -n "$v "; tail -1 gpurun_out/r03/b22.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['p50_ms_unloaded'], d['roofline']['achieved'])"
+done

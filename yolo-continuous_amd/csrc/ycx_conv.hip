@@ -368,6 +368,42 @@ __device__ __forceinline__ void epilogue_regs(const ConvArgs& a, const f32x4 (&a
   }
 }
 
+// act_t over four values with the SiLU's multiplies and add as packed fp32 (v_pk_mul_f32 /
+// v_pk_add_f32, two values per instruction): the same IEEE operations in the same order as
+// act_t, so bit-identical, with half the plain VALU issues beside the exp / rcp. nl2e is
+// -log2(e) held in a VGPR (silu_nl2e()): a packed multiply takes no 32-bit literal.
+__device__ __forceinline__ float silu_nl2e() {
+  float k = -1.44269504f;
+  asm volatile("" : "+v"(k));
+  return k;
+}
+
+template <int ACT>
+__device__ __forceinline__ f32x4 act4_t(f32x4 v, float slope, float nl2e) {
+  if constexpr (ACT == YCX_ACT_SILU) {
+    const f32x4 t = v * nl2e;
+    f32x4 d;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = __builtin_amdgcn_exp2f(t[q]);
+    d = 1.0f + d;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = __builtin_amdgcn_rcpf(d[q]);
+    return v * d;
+  } else {
+    f32x4 r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = act_t<ACT>(v[q], slope);
+    return r;
+  }
+}
+
+// act4_t with the act code at run time (one uniform branch per call)
+__device__ __forceinline__ f32x4 act4(f32x4 v, int act, float slope, float nl2e) {
+  if (act == YCX_ACT_SILU) return act4_t<YCX_ACT_SILU>(v, slope, nl2e);
+  if (act == YCX_ACT_LEAKY) return act4_t<YCX_ACT_LEAKY>(v, slope, nl2e);
+  return v;
+}
+
 // bias8_prefetch loads the bias of these channels (bias is [cout_pad]: always in bounds)
 // before the K loop, so the epilogue does not wait on a load round trip per fragment pair.
 template <int FM>
@@ -409,6 +445,7 @@ __device__ __forceinline__ void epilogue_frag8(const ConvArgs& a, const f32x4 (&
 template <int FM, int FN>
 __device__ __forceinline__ void epilogue_regs8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob, int pxb,
                                                int lane, const f32x4 (&bp)[FM]) {
+  const float nl2e = silu_nl2e();
 #pragma unroll
   for (int k = 0; k < FM / 2; ++k) {
     const int co = cob + 32 * k + 8 * (lane >> 4);
@@ -418,11 +455,14 @@ __device__ __forceinline__ void epilogue_regs8(const ConvArgs& a, const f32x4 (&
     for (int j = 0; j < FN; ++j) {
       const int p = pxb + j * 16 + (lane & 15);
       if (p >= a.M) continue;
+      // bias add and activation as packed fp32 (act4: bit-identical to ycx_act<true>)
+      const f32x4 x0 = act4(acc[2 * k][j] + b0, a.act, a.slope, nl2e);
+      const f32x4 x1 = act4(acc[2 * k + 1][j] + b1, a.act, a.slope, nl2e);
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        v[r] = ycx_act<true>(acc[2 * k][j][r] + b0[r], a.act, a.slope);
-        v[4 + r] = ycx_act<true>(acc[2 * k + 1][j][r] + b1[r], a.act, a.slope);
+        v[r] = x0[r];
+        v[4 + r] = x1[r];
       }
       store8<elt_t>(a, p, co, v);
     }
@@ -2296,7 +2336,9 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
   const int tid = threadIdx.x, lane = tid & 63, lx = lane & 15, kq = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wv & 1, wn = wv >> 1;  // 32-channel half, 2-row half
-  const int tx_n = ca.Wo / kS2TW, tpi = (ca.Ho / kS2TH) * tx_n, ntiles = ca.N * tpi;
+  // tiles run down a column of the image (ty fastest: 0.394 vs 0.415 ms with the packed SiLU;
+  // keeping the shared stem row in LDS for the next tile down measured no faster)
+  const int tx_n = ca.Wo / kS2TW, ty_n = ca.Ho / kS2TH, tpi = ty_n * tx_n, ntiles = ca.N * tpi;
   const int blk = ycx_xcd_remap(blockIdx.x, gridDim.x);
   const int tb = (int)((long long)blk * ntiles / gridDim.x), te = (int)((long long)(blk + 1) * ntiles / gridDim.x);
   if (tb >= te) return;
@@ -2351,8 +2393,8 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)sa.x, (short)0, sa.N * sa.in_cs * HWi * 4, 0x00020000);
   auto fetch = [&](int tile, int buf) {
-    const int n = tile / tpi, ti = tile - n * tpi;
-    const int iy0 = (2 * (ti / tx_n) * kS2TH - 1) * SS - sa.P, ix0 = (2 * (ti % tx_n) * kS2TW - 1) * SS - sa.P;
+    const int n = tile / tpi, ti = tile - n * tpi, tx = ti / ty_n, ty = ti - tx * ty_n;
+    const int iy0 = (2 * ty * kS2TH - 1) * SS - sa.P, ix0 = (2 * tx * kS2TW - 1) * SS - sa.P;
     const int nb = (n * sa.in_cs + sa.in_coff) * HWi;
     char* base = smem + STEM_BYTES + buf * IMGB;
 #pragma unroll
@@ -2383,14 +2425,15 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
     s_dst[u] = ok ? s2_slot(r, c) * 64 + 16 * (kq ^ s2_swz(c >> 1)) : kS2Dump * 64 + 16 * kq;
   }
   fetch(tb, 0);
+  const float nl2e = silu_nl2e();
   elt_t* __restrict__ Y = reinterpret_cast<elt_t*>(ca.y) + ca.out_coff;
   // the previous tile's epilogue issued exactly FM x FN stores per wave after
   // this tile's fetch when every channel is stored (vmcnt counts in issue order)
   const bool exact = ca.Cout == FM * 32;
 
   for (int tile = tb; tile < te; ++tile) {
-    const int n = tile / tpi, ti = tile - n * tpi;
-    const int oy0 = (ti / tx_n) * kS2TH, ox0 = (ti % tx_n) * kS2TW;
+    const int n = tile / tpi, ti = tile - n * tpi, tx = ti / ty_n, ty = ti - tx * ty_n;
+    const int oy0 = ty * kS2TH, ox0 = tx * kS2TW;
     const int sy0 = 2 * oy0 - 1, sx0 = 2 * ox0 - 1;  // stem pixel of tile slot (0, 0)
     const float* img = reinterpret_cast<const float*>(smem + STEM_BYTES + ((tile - tb) & 1) * IMGB);
     if (tile > tb && exact) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FM * FN) : "memory");
@@ -2400,6 +2443,9 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
 
     // (1) stem tile: group g = wv + 4 u covers pixels 16 g .. +15; the MFMA
     //     accumulates onto the bias; branch-free so the unrolled groups overlap
+#ifdef YCX_S2_NOSTEM  // development timing only: the stem phase skipped
+    if (tile < 0)
+#endif
 #pragma unroll
     for (int u = 0; u < GPW; ++u) {
       if (u == GPW - 1 && wv + 4 * u >= NGRP) break;  // uniform: the last group is one wave's
@@ -2410,11 +2456,20 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
       const f32x4 c0 = YCX_MFMA16(af[0], bq, bias_s[0], 0, 0, 0);
       const f32x4 c1 = YCX_MFMA16(af[1], bq, bias_s[1], 0, 0, 0);
       eltx8 o;
+#ifdef YCX_S2_NOACT1  // development timing only (tests/probes/stem2_bench.py): stem without its activation
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        o[q] = (elt_t)act_t<ACT1>(c0[q], sa.slope);
-        o[4 + q] = (elt_t)act_t<ACT1>(c1[q], sa.slope);
+        o[q] = (elt_t)c0[q];
+        o[4 + q] = (elt_t)c1[q];
       }
+#else
+      const f32x4 a0 = act4_t<ACT1>(c0, sa.slope, nl2e), a1 = act4_t<ACT1>(c1, sa.slope, nl2e);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        o[q] = (elt_t)a0[q];
+        o[4 + q] = (elt_t)a1[q];
+      }
+#endif
       *reinterpret_cast<eltx8*>(smem + s_dst[u]) = o;
       if (u & 1) __builtin_amdgcn_sched_barrier(0);  // two groups in flight: bounded registers
     }
@@ -2446,6 +2501,9 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = bvc[i];
+#ifdef YCX_S2_NOCONV  // development timing only: the conv phase's LDS reads and MFMAs skipped
+    if (tile < 0)
+#endif
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int ky = t / 3, kx = t - 3 * ky;
@@ -2470,9 +2528,15 @@ __global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) 
         const int p = n * ca.HoWo + (oy0 + 2 * wn + (j >> 1)) * ca.Wo + ox0 + 16 * (j & 1) + lx;
         float v[8];
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i) {
+#ifdef YCX_S2_NOACT2  // development timing only
+          const f32x4 av = acc[i][j];
+#else
+          const f32x4 av = act4_t<ACT2>(acc[i][j], ca.slope, nl2e);
+#endif
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[4 * i + q] = act_t<ACT2>(acc[i][j][q], ca.slope);
+          for (int q = 0; q < 4; ++q) v[4 * i + q] = av[q];
+        }
         if constexpr (F8) {  // the stem map and this conv run in bf16; only the output is e4m3
           const float sc = ca.out_scale;
           if (YCX_OUT_OK(ca, reinterpret_cast<uint8_t*>(ca.y) + ca.out_coff + (size_t)p * ca.out_cs + co, sizeof(uint2))) *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(ca.y) + ca.out_coff + (size_t)p * ca.out_cs + co) =
