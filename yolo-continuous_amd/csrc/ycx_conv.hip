@@ -420,6 +420,7 @@ __device__ __forceinline__ void bias8_prefetch(const ConvArgs& a, int cob, int l
 template <int FM, int FN>
 __device__ __forceinline__ void epilogue_frag8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob,
                                                const int (&pxf)[FN], int lane, const f32x4 (&bp)[FM]) {
+  const float nl2e = silu_nl2e();
 #pragma unroll
   for (int k = 0; k < FM / 2; ++k) {
     const int co = cob + 32 * k + 8 * (lane >> 4);
@@ -427,11 +428,13 @@ __device__ __forceinline__ void epilogue_frag8(const ConvArgs& a, const f32x4 (&
     const f32x4 b0 = bp[2 * k], b1 = bp[2 * k + 1];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
+      const f32x4 x0 = act4(acc[2 * k][j] + b0, a.act, a.slope, nl2e);
+      const f32x4 x1 = act4(acc[2 * k + 1][j] + b1, a.act, a.slope, nl2e);
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        v[r] = ycx_act<true>(acc[2 * k][j][r] + b0[r], a.act, a.slope);
-        v[4 + r] = ycx_act<true>(acc[2 * k + 1][j][r] + b1[r], a.act, a.slope);
+        v[r] = x0[r];
+        v[4 + r] = x1[r];
       }
       store8<elt_t>(a, pxf[j] + (lane & 15), co, v);
     }
@@ -1801,6 +1804,7 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
   constexpr int HBUF = HPIECES * 1024, WBYTES = 9 * 64 * 128;
   constexpr int FM = 2, FN = 4;
   __shared__ __attribute__((aligned(1024))) char smem[WBYTES + 2 * HBUF];
+  const float nl2e = silu_nl2e();
   char* const wl = smem;
   const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
   const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
@@ -1893,9 +1897,11 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
         const int p = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0 + (lane & 15);
         eltx8 ov;
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i) {
+          const f32x4 x = act4_t<ACT>(acc[i][j], a.slope, nl2e);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)act_t<ACT>(acc[i][j][q], a.slope);
+          for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)x[q];
+        }
         if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov;
       }
     }
