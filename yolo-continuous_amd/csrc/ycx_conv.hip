@@ -1275,6 +1275,7 @@ template <int FM, int FN>
 __device__ __forceinline__ void epilogue_f8x8(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int cob, int pxb,
                                               int lane) {
   const float* dq = a.bias + a.Cout_pad;
+  const float nl2e = silu_nl2e();
   // every bias / dq vector first (bias is [2 cout_pad]: in bounds), one load round trip in all
   f32x4 bb[FM], qq[FM];
 #pragma unroll
@@ -1294,11 +1295,14 @@ __device__ __forceinline__ void epilogue_f8x8(const ConvArgs& a, const f32x4 (&a
     for (int j = 0; j < FN; ++j) {
       const int p = pxb + j * 16 + (lane & 15);
       if (p >= a.M) continue;
+      // dequant-fma and activation as packed fp32 (v_pk_fma_f32, act4): bit-identical
+      const f32x4 x0 = act4(__builtin_elementwise_fma(acc[2 * k][j], q0, b0), a.act, a.slope, nl2e);
+      const f32x4 x1 = act4(__builtin_elementwise_fma(acc[2 * k + 1][j], q1, b1), a.act, a.slope, nl2e);
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        v[r] = ycx_act<true>(fmaf(acc[2 * k][j][r], q0[r], b0[r]), a.act, a.slope);
-        v[4 + r] = ycx_act<true>(fmaf(acc[2 * k + 1][j][r], q1[r], b1[r]), a.act, a.slope);
+        v[r] = x0[r];
+        v[4 + r] = x1[r];
       }
       store8_f8(a, p, co, v);
     }
