@@ -171,6 +171,28 @@ def test_conv_big_tile_residual_up2_slices(device, tile):
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize('tile,cin,cout', [(48, 64, 64), (48, 128, 192), (48, 256, 128), (49, 64, 128),
+                                           (49, 128, 256), (49, 256, 384)])
+def test_conv_halo3x3_band(device, tile, cin, cout):
+    """Band halo tiles (48: 8 x 40, 49: 4 x 40 output rows of a 40-wide map): each lane finds
+    its fragment pixel's (row, column) in the halo; image borders, several 64-channel chunks,
+    channel slices; then a residual and the x2 upsample store."""
+    got, ref = _run_conv(device, 2, 40, 40, cin, cout, 3, 1, L.ACT_SILU, tile, L.DT_BF16, in_extra=8, out_extra=16)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+    got, ref = _run_conv(device, 1, 40, 40, cin, cout, 3, 1, L.ACT_LEAKY, tile, L.DT_BF16, residual=True, seed=1)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=2e-2)
+    got, ref = _run_conv(device, 1, 40, 40, cin, cout, 3, 1, L.ACT_SILU, tile, L.DT_F16, layout=L.OUT_NHWC_UP2,
+                         seed=2)
+    torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3)
+
+
+def test_conv_halo3x3_band_rejects(device):
+    """Band tiles need the map's full width (40) and whole bands of rows."""
+    for tile, hw in ((48, (40, 32)), (48, (36, 40)), (49, (42, 40))):
+        with pytest.raises(L.YcxError, match='unsupported'):
+            _run_conv(device, 1, hw[0], hw[1], 64, 64 if tile == 48 else 128, 3, 1, L.ACT_SILU, tile, L.DT_BF16)
+
+
 def test_conv_halo3x3_residual_up2(device):
     got, ref = _run_conv(device, 1, 32, 16, 64, 64, 3, 1, L.ACT_LEAKY, 19, L.DT_BF16, residual=True)
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=2e-2)

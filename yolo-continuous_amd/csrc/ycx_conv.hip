@@ -1912,14 +1912,21 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
   }
 }
 
-template <int BM, int WM, int WN, int NSTA>
+// TH x TW output tiles. TW = 16: a fragment is one tile row. Band mode (TW != 16, r03): TW is
+// the map's full width (40 at the 40^2 layers), so a tile is TH whole rows whose pixels are
+// consecutive in NHWC; fragment f covers band pixels 16 f .. +15, each lane finds its own
+// (row, column) in the halo, and the epilogue stores 16 consecutive pixels per fragment.
+// tests/probes/conv_bench.py: see DESIGN.md §6 for the band tile against tile 16.
+template <int BM, int WM, int WN, int NSTA, int TH = 16, int TW = 16>
 __global__ void __launch_bounds__(WM * WN * 64) conv3x3_halo(ConvArgs a) {
   constexpr int NW = WM * WN;
-  constexpr int TH = 16, TW = 16, HW = TW + 2, HP = (TH + 2) * HW;  // 324 halo pixels
-  constexpr int HPIECES = (HP + 7) / 8;                             // 1-KB DMA pieces (8 pixels)
-  constexpr int HPW = (HPIECES + NW - 1) / NW;                      // pieces per wave
+  constexpr bool BAND = TW != 16;
+  constexpr int HW = TW + 2, HP = (TH + 2) * HW;  // halo pixels (324 for 16 x 16)
+  constexpr int HPIECES = (HP + 7) / 8;           // 1-KB DMA pieces (8 pixels)
+  constexpr int HPW = (HPIECES + NW - 1) / NW;    // pieces per wave
   constexpr int TM = BM / WM, FM = TM / 16;
-  constexpr int FN = TH / WN;  // tile rows (16-pixel fragments) per wave
+  constexpr int FN = TH * TW / 16 / WN;  // 16-pixel fragments per wave
+  static_assert(TH * TW % (16 * WN) == 0, "whole fragments per wave");
   constexpr int A_BYTES = BM * 64 * 2, A_PW = BM / (8 * NW);
   static_assert(A_PW >= 1 && BM % (8 * NW) == 0, "A rows per wave");
   __shared__ __attribute__((aligned(1024))) char smem[NSTA * A_BYTES + HPIECES * 1024];
@@ -1936,6 +1943,13 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3x3_halo(ConvArgs a) {
   const int oy0 = (ti / tx_n) * TH, ox0 = (ti % tx_n) * TW, co0 = ct * BM;
   const int lrow = lane >> 3, pch = lane & 7;
   const int w_bytes = a.Cout_pad * a.Ktot * 2, x_bytes = a.N * a.H * a.W * a.in_cs * 2;
+  // band mode: halo pixel of fragment j's lane at tap (0, 0)
+  int hb[BAND ? FN : 1];
+#pragma unroll
+  for (int j = 0; j < (BAND ? FN : 1); ++j) {
+    const int q = 16 * (wn * FN + j) + (lane & 15);
+    hb[j] = (q / TW) * HW + q % TW;
+  }
 
   // permuted A rows as in conv_bf16_glds: 16-byte epilogue stores
   int a_off[A_PW];
@@ -2008,7 +2022,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3x3_halo(ConvArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int h = (wn * FN + j + ky) * HW + (lane & 15) + kx;
+        const int h = BAND ? hb[j] + ky * HW + kx : (wn * FN + j + ky) * HW + (lane & 15) + kx;
         bfr[j] = *reinterpret_cast<const eltx8*>(halo + h * 128 + ((lc ^ (h & 7)) << 4));
       }
 #pragma unroll
@@ -2021,7 +2035,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3x3_halo(ConvArgs a) {
   }
   int pxf[FN];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) pxf[j] = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0;
+  for (int j = 0; j < FN; ++j)
+    pxf[j] = BAND ? n * a.HoWo + oy0 * a.Wo + 16 * (wn * FN + j) : n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0;
   if constexpr (FM % 2 == 0) {
     f32x4 bpre[FM];  // loaded here: prefetched before the K loop it cost this kernel 8-15 %
     bias8_prefetch<FM>(a, co0 + wm * TM, lane, bpre);
@@ -3061,6 +3076,8 @@ const TileInfo kTiles[] = {
     {256, 128, 32, "big_co256_px128_k32_s3_dma_mid_mfma"},
     {256, 128, 32, "big_co256_px128_k32_s3_dma_after_mfma"},
     {256, 256, 32, "big_co256_px256_k32_s4_dma_after_mfma"},
+    {64, 320, 64, "halo3x3_band_co64_8x40_s2"},
+    {128, 160, 64, "halo3x3_band_co128_4x40_s2"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -3093,14 +3110,15 @@ ycx_status launch_ws64(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
-template <int BM, int WM, int WN, int NSTA>
+template <int BM, int WM, int WN, int NSTA, int TH = 16, int TW = 16>
 ycx_status launch_halo(ConvArgs a, hipStream_t st) {
-  if (a.KH != 3 || a.KW != 3 || a.S != 1 || a.P != 1 || a.H != a.Ho || a.W != a.Wo || a.Ho % 16 || a.Wo % 16 ||
-      a.Cin % 64 || a.Cout_pad % BM || a.out_layout == YCX_OUT_NCHW_F32)
+  constexpr bool BAND = TW != 16;
+  if (a.KH != 3 || a.KW != 3 || a.S != 1 || a.P != 1 || a.H != a.Ho || a.W != a.Wo || a.Ho % TH ||
+      (BAND ? a.Wo != TW : a.Wo % TW != 0) || a.Cin % 64 || a.Cout_pad % BM || a.out_layout == YCX_OUT_NCHW_F32)
     return YCX_ERR_UNSUPPORTED;
   a.n_ct = a.Cout_pad / BM;
-  a.nwg = a.n_ct * a.N * (a.Ho / 16) * (a.Wo / 16);
-  hipLaunchKernelGGL((conv3x3_halo<BM, WM, WN, NSTA>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
+  a.nwg = a.n_ct * a.N * (a.Ho / TH) * (a.Wo / TW);
+  hipLaunchKernelGGL((conv3x3_halo<BM, WM, WN, NSTA, TH, TW>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
   return ycx_launch_status();
 }
 
@@ -3365,6 +3383,12 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
     if (d->cout_pad % 128 == 0) return 20;
     if (d->cout_pad == 64 && d->ho >= 160) return 19;
   }
+  // 40-wide maps (not 16-aligned): the 8 x 40 band halo tile where it has >= 2.5 waves of
+  // workgroups (40^2 bs 32 256->512: 0.113 vs 0.124 ms; with fewer workgroups it loses to tile 16,
+  // profiles/r03/band_halo_40.txt)
+  if (d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->h == d->ho && d->w == d->wo && d->wo == 40 &&
+      d->ho % 8 == 0 && d->out_layout != YCX_OUT_NCHW_F32 && (long long)(d->cout_pad / 64) * d->n * (d->ho / 8) >= 1280)
+    return 48;
   if (d->cout_pad % 128 == 0) {
     if ((d->cout_pad / 128) * ((M + 127) / 128) >= 256) return 16;
     // small-M (deep) layers: co64 x px128 LDS-DMA blocks, two per CU (tests/probes/conv_bench.py,
@@ -3498,6 +3522,8 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x,
     case 45: return launch_bigt<256, 128, 4, 2, 3, 2>(a, st);
     case 46: return launch_bigt<256, 128, 4, 2, 3, 3>(a, st);
     case 47: return launch_bigt<256, 256, 4, 4, 4, 3>(a, st);  // tile 40 likewise
+    case 48: return launch_halo<64, 2, 4, 2, 8, 40>(a, st);      // band halo tiles (40-wide maps)
+    case 49: return launch_halo<128, 4, 2, 2, 4, 40>(a, st);
 #ifdef YCX_EXPERIMENTAL_TILES  // retired experiments (tools/build_variant.sh NAME -DYCX_EXPERIMENTAL_TILES)
     case 27: return launch_p8<256, 256>(a, st);
     case 28: return launch_p8<128, 256>(a, st);
