@@ -1294,9 +1294,14 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
 // ---------------------------------------------------------------------------
 // The LDS-resident classes (S <= kFastMax and fast_lds_bytes(S) fits): big_fast, one
 // 1024-thread workgroup per class (grid-strided task loop); nms_big then takes the rest.
+__device__ __attribute__((noinline)) void wide_a_task(const ycx_nms_desc& d, const ycx_cand* __restrict__ cand, char* ws,
+                                            const Layout& L, int t, const Task& tk, char* smem, int (*s_lv)[5],
+                                            int* s_ext, int* s_w, unsigned long long* s_msk, int all_pairs);
+
 template <int E>  // one launch per register-array width: each instance allocates its own registers
 __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_fast(
-    ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws, Thr thr, float t_lo, float inv_t, int all_pairs) {
+    ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws, Thr thr, float t_lo, float inv_t, int all_pairs,
+    int with_wide) {
   __shared__ __attribute__((aligned(16))) char smem[kBigLds];
   __shared__ int s_lv[kFLevels][5];
   __shared__ int s_ext[4];
@@ -1309,8 +1314,18 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   const Layout L = layout(d.n, rows);
   const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
   const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks);
-  const int ntasks = hdr->ntasks;
-  for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
+  const int ntasks = hdr->ntasks, nwide = with_wide ? hdr->nwide : 0;
+  // the wide classes' sort + spatial index first (the longest items), then the fast classes
+  for (int w = blockIdx.x; w < nwide + ntasks; w += gridDim.x) {
+    if (w < nwide) {
+      constexpr int kCellB = ((kFCells * 4) + 255) & ~255;  // u32 cell ends
+      static_assert(kBigLds >= 16 * (kMaxRows / kBigThreads) * (kBigThreads / 64) * 4 && kBigLds >= kCellB + 1024,
+                    "wide path LDS: radix counts, cells");
+      const Task* wt = tasks + (size_t)d.n * L.max_tasks;  // the wide list
+      wide_a_task(d, cand, ws, L, w, wt[w], smem, s_lv, s_ext, s_w, s_msk, all_pairs);
+      continue;
+    }
+    const int t = w - nwide;
     const Task tk = tasks[t];
 
     const Ptrs P = image_ptrs(ws, L, tk.img);
@@ -1449,26 +1464,15 @@ __device__ unsigned long long* radix_sort_global(unsigned long long* a, unsigned
   return a;
 }
 
-__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_wide_a(
-    ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws, Thr thr, float t_lo, float inv_t, int all_pairs) {
-  constexpr int kCellB = ((kFCells * 4) + 255) & ~255;  // u32 cell ends
-  static_assert(kBigLds >= 16 * (kMaxRows / kBigThreads) * (kBigThreads / 64) * 4 && kBigLds >= kCellB + 1024,
-                "wide path LDS: radix counts, cells");
-  __shared__ __attribute__((aligned(16))) char smem[kBigLds];
-  __shared__ int s_lv[kFLevels][5];
-  __shared__ int s_ext[4];
-  __shared__ int s_w[kBigThreads / 64];
-  __shared__ unsigned long long s_msk[2];
+// nms_wide_a's work for wide task t: the class's keys sorted, boxes in rank order, the
+// spatial index published for nms_wide_s / nms_wide_b (run inside nms_fast's launch, beside
+// the fast classes: both are one workgroup per class and neither waits on the other)
+__device__ __attribute__((noinline)) void wide_a_task(const ycx_nms_desc& d, const ycx_cand* __restrict__ cand, char* ws,
+                                            const Layout& L, int t, const Task& tk, char* smem, int (*s_lv)[5],
+                                            int* s_ext, int* s_w, unsigned long long* s_msk, int all_pairs) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int rows = d.rows_total;
-  const Layout L = layout(d.n, rows);
-  const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
-  const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks);
-  const int ntasks = hdr->nwide;
-  tasks += (size_t)d.n * L.max_tasks;  // the wide list
   unsigned* cells = reinterpret_cast<unsigned*>(smem);
-  for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
-    const Task tk = tasks[t];
     const int S = tk.S, off = tk.off;
     const Ptrs P = image_ptrs(ws, L, tk.img);
     const ycx_cand* ci = cand + (size_t)tk.img * rows;
@@ -1607,7 +1611,6 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
     if (tid < kFLevels * 5) fr->lv[tid / 5][tid % 5] = s_lv[tid / 5][tid % 5];
     YCX_WPROF_MARK(1)
     __syncthreads();
-  }
 }
 
 constexpr int kWChunk = 2048;  // positions per nms_wide_s item
@@ -2038,15 +2041,16 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   const float t_lo = all_pairs ? 0.0f : (float)(fmin(d->iou_thres, 1.0) * (1.0 - 1e-3));
   const float inv_t = t_lo > 0.0f ? 1.0f / t_lo : INFINITY;
   hipLaunchKernelGGL(nms_prep, dim3(d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws, t);
-#ifndef YCX_NMS_NO_FAST
   // one width for every fast class: the radix sort and the per-element loops skip the
-  // elements past S, so E = 8 costs a small class little, and one launch replaces four
-  hipLaunchKernelGGL(nms_fast<8>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
-#endif
+  // elements past S, so E = 8 costs a small class little, and one launch replaces four;
+  // with the wide classes' sort + spatial index (nms_wide_a's work) in the same launch: at C4
+  // the 24 wide and 24 fast classes of a batch then run side by side instead of in turn
+  // (YCX_NMS_NO_FAST: every class on the wide path, the fast list empty)
 #ifdef YCX_NMS_OLD_BIG  // development A/B: the r02 general path for every class the fast path leaves
+  hipLaunchKernelGGL(nms_fast<8>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs, 0);
   hipLaunchKernelGGL(nms_big, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
 #else
-  hipLaunchKernelGGL(nms_wide_a, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
+  hipLaunchKernelGGL(nms_fast<8>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs, 1);
   hipLaunchKernelGGL(nms_wide_s, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
   hipLaunchKernelGGL(nms_wide_b, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
 #endif
