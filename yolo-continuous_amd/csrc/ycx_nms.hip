@@ -2,13 +2,14 @@
 // loop of detect.py:124-137 (unique classes ascending, nms per class, results
 // concatenated class by class) for the whole batch in three launches.
 //
-//  nms_prep    one 1024-thread workgroup per image: class histogram (LDS
-//              atomics) + exclusive scan -> one bucket per class; every wave
-//              pulls whole classes from an LDS counter and a class of S <= 512
+//  nms_count / nms_bucket / nms_prep   16 workgroups per image: class histograms
+//              of candidate slices, exclusive scan -> one bucket per class; every
+//              wave pulls whole classes from an LDS counter and a class of S <= 512
 //              candidates is finished entirely in registers (64*R keys
 //              bitonic-sorted across lanes and register slots, greedy scan with
 //              removed/kept bit masks, box i broadcast by readlane). Larger
-//              classes are queued as tasks for nms_big.
+//              classes are queued as tasks (nms_fast / nms_wide, below; the r02
+//              general path nms_big under -DYCX_NMS_OLD_BIG).
 //  nms_big     one 1024-thread workgroup per large class (grid-strided task
 //              loop). (1) score sort (score desc, row asc = torchvision's stable
 //              descending order) -> rank. (2) spatial counting sort: level =
@@ -89,8 +90,17 @@ struct Task {  // one large class
   int img, cls, off, S;
 };
 
+constexpr int kPrepB = 16;  // workgroups per image in the class bucketing (nms_count / nms_bucket)
+#ifndef YCX_PREP_CLS_B
+#define YCX_PREP_CLS_B 4
+#endif
+// workgroups per image over the classes (nms_prep): 4 measured best of 1 / 4 / 16 (dense
+// G3 load 24.0k -> 58.9k img/s decode + NMS; C2 neutral; C4 +1.3 %; 16: C2 post 0.51 -> 0.57 ms)
+constexpr int kPrepClsB = YCX_PREP_CLS_B;
+
 struct Layout {
-  size_t hdr, tasks, wframes, wcells, per_image_base;  // header + task tables + wide-class index (batch), then per image:
+  size_t hdr, tasks, wframes, wcells, bcnt, per_image_base;  // header + task tables + wide-class index +
+                                                             // slice class counts (batch), then per image:
   size_t keys, bucket, kept, sbox, srank, nsup, slots, state, cnt, offs, kc, per_image;
   int max_tasks, max_wide;  // big classes per image; wide classes per image
 };
@@ -116,7 +126,8 @@ __host__ __device__ inline Layout layout(int n, int rows) {
   L.max_wide = rows / wide_min_s() + 1;
   L.wframes = al(L.tasks + 2 * (size_t)n * L.max_tasks * sizeof(Task));  // fast list, then wide list
   L.wcells = al(L.wframes + (size_t)n * L.max_wide * wframe_bytes());
-  L.per_image_base = al(L.wcells + (size_t)n * L.max_wide * wide_cells_bytes());
+  L.bcnt = al(L.wcells + (size_t)n * L.max_wide * wide_cells_bytes());
+  L.per_image_base = al(L.bcnt + (size_t)n * kPrepB * kMaxNc * 4);
   size_t o = 0;
   // keys: a class at bucket offset `off` with S rows sorts at keys + 2*off; its
   // power-of-two span is < 2S and off + S <= rows, so 2*rows keys suffice.
@@ -400,65 +411,119 @@ __device__ __forceinline__ Ptrs image_ptrs(char* ws, const Layout& L, int img) {
 }
 
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) nms_prep(ycx_nms_desc d, const ycx_cand* __restrict__ cand,
-                                                     const int* __restrict__ cand_rows,
-                                                     const int* __restrict__ cand_counts, char* ws, Thr thr) {
-  __shared__ int s_cnt[kMaxNc], s_off[kMaxNc], s_fill[kMaxNc], s_kc[kMaxNc];
+// Class bucketing of each image's candidates, on kPrepB workgroups per image (one per
+// image took 0.19 ms per batch at C2 and 0.36 ms at C4, 8 workgroups on the whole chip):
+// nms_count histograms slice b of the candidate list per class; nms_bucket places the
+// slice's rows at class offset + the earlier slices' counts (an LDS atomic within the
+// slice: the order inside a class bucket is free, every consumer sorts by (score, row));
+// nms_prep then finishes the small classes and lists the big ones, classes c = b mod kPrepB
+// on workgroup b.
+__device__ __forceinline__ void prep_slice(int cnt, int b, int& i0, int& i1) {
+  i0 = (int)((long long)cnt * b / kPrepB);
+  i1 = (int)((long long)cnt * (b + 1) / kPrepB);
+}
+
+__global__ void __launch_bounds__(kThreads) nms_count(ycx_nms_desc d, const ycx_cand* __restrict__ cand,
+                                                      const int* __restrict__ cand_rows,
+                                                      const int* __restrict__ cand_counts, char* ws) {
+  __shared__ int s_cnt[kMaxNc];
+  const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  const int nc = d.nc, rows = d.rows_total;
+  const Layout L = layout(d.n, rows);
+  const ycx_cand* ci = cand + (size_t)img * rows;
+  const int* cr = cand_rows + (size_t)img * rows;
+  int i0, i1;
+  prep_slice(min(cand_counts[img], rows), b, i0, i1);
+  for (int c = tid; c < nc; c += kThreads) s_cnt[c] = 0;
+  __syncthreads();
+  for (int i = i0 + tid; i < i1; i += kThreads) atomicAdd(&s_cnt[ci[cr[i]].cls], 1);
+  __syncthreads();
+  int* bc = reinterpret_cast<int*>(ws + L.bcnt) + ((size_t)img * kPrepB + b) * kMaxNc;
+  for (int c = tid; c < nc; c += kThreads) bc[c] = s_cnt[c];
+}
+
+__global__ void __launch_bounds__(kThreads) nms_bucket(ycx_nms_desc d, const ycx_cand* __restrict__ cand,
+                                                       const int* __restrict__ cand_rows,
+                                                       const int* __restrict__ cand_counts, char* ws) {
+  __shared__ int s_cnt[kMaxNc], s_off[kMaxNc], s_base[kMaxNc], s_fill[kMaxNc];
+  const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, wid = tid >> 6;
+  const int nc = d.nc, rows = d.rows_total;
+  const Layout L = layout(d.n, rows);
+  const Ptrs P = image_ptrs(ws, L, img);
+  const ycx_cand* ci = cand + (size_t)img * rows;
+  const int* cr = cand_rows + (size_t)img * rows;
+  const int* bc = reinterpret_cast<const int*>(ws + L.bcnt) + (size_t)img * kPrepB * kMaxNc;
+  for (int c = tid; c < nc; c += kThreads) {
+    int tot = 0, before = 0;
+    for (int q = 0; q < kPrepB; ++q) {
+      const int v = bc[(size_t)q * kMaxNc + c];
+      before += q < b ? v : 0;
+      tot += v;
+    }
+    s_cnt[c] = tot;
+    s_base[c] = before;
+    s_fill[c] = 0;
+  }
+  __syncthreads();
+  if (wid == 0) wave_exclusive_scan(s_cnt, s_off, nc);
+  __syncthreads();
+  if (b == 0)
+    for (int c = tid; c < nc; c += kThreads) {
+      P.cnt[c] = s_cnt[c];
+      P.offs[c] = s_off[c];
+    }
+  int i0, i1;
+  prep_slice(min(cand_counts[img], rows), b, i0, i1);
+  for (int i = i0 + tid; i < i1; i += kThreads) {
+    const int r = cr[i];
+    const int c = ci[r].cls;
+    P.bucket[s_off[c] + s_base[c] + atomicAdd(&s_fill[c], 1)] = r;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) nms_prep(ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws,
+                                                     Thr thr) {
+  __shared__ int s_kc[kMaxNc];
   __shared__ int s_next;
-  const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int nc = d.nc, rows = d.rows_total;
   const Layout L = layout(d.n, rows);
   const Ptrs P = image_ptrs(ws, L, img);
   Hdr* hdr = reinterpret_cast<Hdr*>(ws + L.hdr);
   Task* tasks = reinterpret_cast<Task*>(ws + L.tasks);
   const ycx_cand* ci = cand + (size_t)img * rows;
-  const int* cr = cand_rows + (size_t)img * rows;
-  const int cnt = min(cand_counts[img], rows);
+  const int nown = (nc - b + kPrepClsB - 1) / kPrepClsB;  // classes b, b + kPrepClsB, ...
 
-  for (int c = tid; c < nc; c += kThreads) { s_cnt[c] = 0; s_fill[c] = 0; s_kc[c] = 0; }
+  for (int k = tid; k < nown; k += kThreads) s_kc[k] = 0;
   if (tid == 0) s_next = 0;
   __syncthreads();
-  for (int i = tid; i < cnt; i += kThreads) atomicAdd(&s_cnt[ci[cr[i]].cls], 1);
-  __syncthreads();
-  if (wid == 0) wave_exclusive_scan(s_cnt, s_off, nc);
-  __syncthreads();
-  for (int i = tid; i < cnt; i += kThreads) {
-    const int r = cr[i];
-    const int c = ci[r].cls;
-    P.bucket[s_off[c] + atomicAdd(&s_fill[c], 1)] = r;
-  }
-  __syncthreads();
-
   // Classes of <= kRegMax candidates: one wave each, in registers; larger
-  // classes become nms_big tasks.
-  for (int it = 0; it <= nc + 64; ++it) {  // bounded work-queue loop
-    int c = 0;
-    if (lane == 0) c = atomicAdd(&s_next, 1);
-    c = __builtin_amdgcn_readfirstlane(__shfl(c, 0));
-    if (c >= nc) break;
-    const int S = __builtin_amdgcn_readfirstlane(s_cnt[c]);
+  // classes become nms_fast / nms_wide tasks.
+  for (int it = 0; it <= nown + 64; ++it) {  // bounded work-queue loop
+    int k = 0;
+    if (lane == 0) k = atomicAdd(&s_next, 1);
+    k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
+    if (k >= nown) break;
+    const int c = b + k * kPrepClsB;
+    const int S = __builtin_amdgcn_readfirstlane(P.cnt[c]), off = __builtin_amdgcn_readfirstlane(P.offs[c]);
     if (S == 0) continue;
     if (S > kRegMax) {
       if (lane == 0) {
-        if (fast_task(S)) tasks[atomicAdd(&hdr->ntasks, 1)] = Task{img, c, s_off[c], S};
-        else tasks[(size_t)d.n * L.max_tasks + atomicAdd(&hdr->nwide, 1)] = Task{img, c, s_off[c], S};
+        if (fast_task(S)) tasks[atomicAdd(&hdr->ntasks, 1)] = Task{img, c, off, S};
+        else tasks[(size_t)d.n * L.max_tasks + atomicAdd(&hdr->nwide, 1)] = Task{img, c, off, S};
       }
       continue;
     }
-    const int* bk = P.bucket + s_off[c];
-    int* kp = P.kept + s_off[c];
-    if (S <= 64) class_in_registers<1>(ci, bk, kp, S, thr, &s_kc[c]);
-    else if (S <= 128) class_in_registers<2>(ci, bk, kp, S, thr, &s_kc[c]);
-    else if (S <= 256) class_in_registers<4>(ci, bk, kp, S, thr, &s_kc[c]);
-    else class_in_registers<8>(ci, bk, kp, S, thr, &s_kc[c]);
+    const int* bk = P.bucket + off;
+    int* kp = P.kept + off;
+    if (S <= 64) class_in_registers<1>(ci, bk, kp, S, thr, &s_kc[k]);
+    else if (S <= 128) class_in_registers<2>(ci, bk, kp, S, thr, &s_kc[k]);
+    else if (S <= 256) class_in_registers<4>(ci, bk, kp, S, thr, &s_kc[k]);
+    else class_in_registers<8>(ci, bk, kp, S, thr, &s_kc[k]);
   }
   __syncthreads();
-  // Per-image class tables (nms_big overwrites kc of its classes).
-  for (int c = tid; c < nc; c += kThreads) {
-    P.cnt[c] = s_cnt[c];
-    P.offs[c] = s_off[c];
-    P.kc[c] = s_kc[c];
-  }
+  // this workgroup's classes' kept counts (nms_fast / nms_wide overwrite kc of theirs)
+  for (int k = tid; k < nown; k += kThreads) P.kc[b + k * kPrepClsB] = s_kc[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -2040,7 +2105,9 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   const int all_pairs = !(d->iou_thres >= 0.0);
   const float t_lo = all_pairs ? 0.0f : (float)(fmin(d->iou_thres, 1.0) * (1.0 - 1e-3));
   const float inv_t = t_lo > 0.0f ? 1.0f / t_lo : INFINITY;
-  hipLaunchKernelGGL(nms_prep, dim3(d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws, t);
+  hipLaunchKernelGGL(nms_count, dim3(kPrepB, d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws);
+  hipLaunchKernelGGL(nms_bucket, dim3(kPrepB, d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws);
+  hipLaunchKernelGGL(nms_prep, dim3(kPrepClsB, d->n), dim3(kThreads), 0, st, *d, cand, ws, t);
   // one width for every fast class: the radix sort and the per-element loops skip the
   // elements past S, so E = 8 costs a small class little, and one launch replaces four;
   // with the wide classes' sort + spatial index (nms_wide_a's work) in the same launch: at C4
