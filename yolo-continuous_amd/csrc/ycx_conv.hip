@@ -2901,11 +2901,15 @@ __global__ void __launch_bounds__(512) conv3x3_ws64_f8(ConvArgs a) {
   if (tb >= te) return;
   const int w_bytes = a.Cout_pad * a.Ktot, x_bytes = a.N * a.H * a.W * a.in_cs;
 
-  // weights: LDS row R = 64 step + co (128 B), logical chunk q at q ^ swz(co); 40 pieces, 5 per wave
+  // weights: LDS row R = 64 step + co (128 B), logical chunk q at q ^ swz(co); 40 pieces, 5 per wave.
+  // Row co holds channel 32 (co >> 5) + 8 (m >> 2) + 4 f + (m & 3) (f = co >> 4 & 1, m = co & 15), as in
+  // conv3x3_ws64: C rows 4g..4g+3 of the two fragments are channels 32 wm + 8g .. +7, one 8-byte store
+  // per lane and pixel
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    const int R = 8 * (wid + NW * i) + lrow, st = R >> 6, co = R & 63;
-    buf_lds16(Wt, w_bytes, co * a.Ktot + st * 128 + ((pch ^ swz8(co)) << 4), 0, wl + (wid + NW * i) * 1024);
+    const int R = 8 * (wid + NW * i) + lrow, st = R >> 6, co = R & 63, m = co & 15;
+    const int ch = (co & 32) + 8 * (m >> 2) + 4 * ((co >> 4) & 1) + (m & 3);
+    buf_lds16(Wt, w_bytes, ch * a.Ktot + st * 128 + ((pch ^ swz8(co)) << 4), 0, wl + (wid + NW * i) * 1024);
   }
   // halo of a tile into buffer b: a 1-KB piece is 16 pixels; lane -> pixel (lane >> 2), physical chunk lane & 3
   auto issue_h = [&](int tile, int b) {
@@ -2927,12 +2931,13 @@ __global__ void __launch_bounds__(512) conv3x3_ws64_f8(ConvArgs a) {
   f32x4 bv[FM], qv[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int co = 32 * wm + 16 * i + 4 * (lane >> 4);
+    const int co = 32 * wm + 8 * (lane >> 4) + 4 * i;
     const bool ok = co < a.Cout;
     bv[i] = ok ? *reinterpret_cast<const f32x4*>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
     qv[i] = ok ? *reinterpret_cast<const f32x4*>(a.bias + a.Cout_pad + co) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const bool exact = a.Cout == 64;  // then every tile stores FM x FN times per wave
+  const float nl2e = silu_nl2e();
+  const bool exact = a.Cout == 64;  // then every tile stores FN times per wave
   uint8_t* __restrict__ Y = reinterpret_cast<uint8_t*>(a.y) + a.out_coff;
   const float osc = a.out_scale;
   const int g = lane >> 4, c0 = 2 * g;   // A: chunk pair of the 128-B row
@@ -2940,7 +2945,7 @@ __global__ void __launch_bounds__(512) conv3x3_ws64_f8(ConvArgs a) {
 
   for (int tile = tb; tile < te; ++tile) {
     const int b = (tile - tb) & 1;
-    if (tile > tb && exact) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FM * FN) : "memory");
+    if (tile > tb && exact) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FN) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // this tile's halo (and the weights) landed; the other buffer is free
     if (tile + 1 < te) issue_h(tile + 1, b ^ 1);
@@ -2980,20 +2985,20 @@ __global__ void __launch_bounds__(512) conv3x3_ws64_f8(ConvArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
       __builtin_amdgcn_sched_barrier(0);  // one step's fragments live at a time
     }
-    // epilogue: e4m3 4-byte stores from registers (no global loads: they would drain vmcnt)
+    // epilogue: e4m3 8-byte stores (8 consecutive channels per lane and pixel) from registers
+    // (no global loads: they would drain vmcnt); dequant-fma and act as packed fp32
     const int n = tile / tpi, ti = tile - n * tpi;
     const int oy0 = (ti / tx_n) * TH, ox0 = (ti % tx_n) * TW;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int co = 32 * wm + 16 * i + 4 * (lane >> 4);
-      if (co >= a.Cout) continue;
+    const int co = 32 * wm + 8 * (lane >> 4);
+    if (co < a.Cout) {  // cout % 8 == 0: the 8 channels are all valid
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int p = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0 + (lane & 15);
-        float v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = act_t<ACT>(fmaf(acc[i][j][q], qv[i][q], bv[i][q]), a.slope) * osc;
-        if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(uint32_t))) *reinterpret_cast<uint32_t*>(Y + (size_t)p * a.out_cs + co) = f8x4_pack(v[0], v[1], v[2], v[3]);
+        const f32x4 x0 = act4_t<ACT>(__builtin_elementwise_fma(acc[0][j], qv[0], bv[0]), a.slope, nl2e) * osc;
+        const f32x4 x1 = act4_t<ACT>(__builtin_elementwise_fma(acc[1][j], qv[1], bv[1]), a.slope, nl2e) * osc;
+        if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(uint2)))
+          *reinterpret_cast<uint2*>(Y + (size_t)p * a.out_cs + co) =
+              make_uint2(f8x4_pack(x0[0], x0[1], x0[2], x0[3]), f8x4_pack(x1[0], x1[1], x1[2], x1[3]));
       }
     }
   }
