@@ -157,6 +157,29 @@ def test_conv3x3_ws64(device, n, hw, cout, act):
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize('n,hw,cout,act,dt', [(2, (32, 64), 128, L.ACT_SILU, L.DT_BF16),
+                                              (1, (31, 63), 96, L.ACT_LEAKY, L.DT_BF16),
+                                              (3, (256, 160), 128, L.ACT_SILU, L.DT_BF16),
+                                              (2, (64, 32), 128, L.ACT_NONE, L.DT_F16),
+                                              (3, (256, 160), 120, L.ACT_SILU, L.DT_F16)])
+def test_conv3x3s2_wsr(device, n, hw, cout, act, dt):
+    """3x3/s2 64 -> 128 with weights in registers (tile 50): parity-split halo columns, image
+    borders (odd input sizes too), several tiles per persistent block (480 tiles on <= 256
+    blocks), cout < cout_pad, channel-sliced input/output."""
+    got, ref = _run_conv(device, n, hw[0], hw[1], 64, cout, 3, 2, act, 50, dt, in_extra=8, out_extra=16)
+    tol = 1e-2 if dt == L.DT_BF16 else 2e-3
+    torch.testing.assert_close(got, ref, rtol=tol, atol=tol)
+
+
+def test_conv3x3s2_wsr_rejects(device):
+    """Tile 50 needs cin 64, cout_pad 128, stride 2 and Wo % 16 == Ho % 4 == 0."""
+    for args in ((2, 32, 40, 64, 128, 3, 2), (2, 32, 64, 128, 128, 3, 2), (2, 32, 64, 64, 256, 3, 2),
+                 (2, 30, 64, 64, 128, 3, 2), (2, 32, 64, 64, 128, 3, 1)):
+        n, h, w, cin, cout, k, s = args
+        with pytest.raises(L.YcxError, match='unsupported'):
+            _run_conv(device, n, h, w, cin, cout, k, s, L.ACT_SILU, 50, L.DT_BF16)
+
+
 @pytest.mark.parametrize('tile', [40, 41, 42, 43, 44, 45, 46, 47])
 def test_conv_big_tile_residual_up2_slices(device, tile):
     """Tiles 40-43 (conv_bigt, 32-deep K stages): residual add, x2 upsample store, channel

@@ -1912,6 +1912,135 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
   }
 }
 
+// -------------------------------------------------------------------------
+// 3x3/s2 conv, 64 -> <= 128 channels, weights in VGPRs (tile 50: yolov7's 320^2 -> 160^2
+// 64 -> 128 downsample). The im2col tile 16 pulls every input pixel through LDS ~2.25
+// times plus the whole 147 KB weight tensor per 128-pixel tile (~2.3 KB of LDS-DMA per
+// output pixel). Here one 512-thread block per CU keeps each wave's 32 output channels x
+// 576 K of weights in registers (36 A fragments) across a contiguous range of TH x 16
+// output tiles and DMAs only each tile's (2 TH + 1) x 33 input halo (594 B per output pixel
+// at TH = 4),
+// double-buffered as in conv3x3_ws64. Halo columns are stored split by parity (the 17
+// even columns, then the 16 odd ones), so at every tap a fragment's 16 output pixels
+// read 16 consecutive halo slots; slot h keeps chunk q at q ^ (h & 7).
+// Wave (wm, wn): channels 32 wm .. +31, tile rows TH / 2 * wn .. +TH / 2. TH = 4 keeps the
+// 144 weight VGPRs, 16 accumulators and 8 B fragments under the 256 registers of two waves
+// per SIMD (TH = 8 spills).
+// Requires Cin == 64, Cout_pad == 128, pad 1, Ho % TH == Wo % 16 == 0, NHWC output
+// without residual.
+// -------------------------------------------------------------------------
+template <int ACT, int TH>
+__global__ void __launch_bounds__(512) conv3x3s2_wsr(ConvArgs a) {
+  constexpr int NW = 8, TW = 16, HC = 2 * TW + 1, HP = (2 * TH + 1) * HC;  // 17 x 33 halo pixels
+  constexpr int HEVEN = TW + 1;                                                   // even columns: slots 0..16
+  constexpr int HPIECES = (HP + 7) / 8, HPW = (HPIECES + NW - 1) / NW;           // 1-KB DMA pieces (8 pixels)
+  constexpr int HBUF = HPIECES * 1024;
+  constexpr int FM = 2, FN = TH / 2;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * HBUF];
+  const float nl2e = silu_nl2e();
+  const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
+  const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int tx_n = a.Wo / TW, tpi = (a.Ho / TH) * tx_n, ntiles = a.N * tpi;
+  const int blk = ycx_xcd_remap(blockIdx.x, gridDim.x);
+  const int tb = (int)((long long)blk * ntiles / gridDim.x), te = (int)((long long)(blk + 1) * ntiles / gridDim.x);
+  if (tb >= te) return;
+  const int x_bytes = a.N * a.H * a.W * a.in_cs * 2;
+
+  auto issue_h = [&](int tile, int b) {
+    const int n = tile / tpi, ti = tile - n * tpi;
+    const int iy0 = 2 * (ti / tx_n) * TH - 1, ix0 = 2 * (ti % tx_n) * TW - 1;
+#pragma unroll
+    for (int i = 0; i < HPW; ++i) {
+      const int piece = wid + NW * i;
+      if (piece >= HPIECES) break;  // uniform
+      const int h = 8 * piece + lrow, hy = h / HC, s = h - hy * HC;
+      const int iy = iy0 + hy, ix = ix0 + (s < HEVEN ? 2 * s : 2 * (s - HEVEN) + 1);
+      const bool ok = h < HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      buf_lds16(X, x_bytes, ok ? (((n * a.H + iy) * a.W + ix) * a.in_cs + a.in_coff + ((pch ^ (h & 7)) << 3)) * 2
+                               : 0x7FFFFFF0, 0, smem + b * HBUF + piece * 1024);
+    }
+  };
+  issue_h(tb, 0);
+  // A fragments of all nine taps: row m of fragment i is channel 32 wm + 8 (m >> 2) + 4 i + (m & 3),
+  // so C rows 4g..4g+3 of the two fragments are channels 32 wm + 8g .. +7 (one 16-byte store per lane)
+  eltx8 wf[9][2][FM];
+  {
+    const int m = lane & 15;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const elt_t* wr = Wt + (size_t)(32 * wm + 8 * (m >> 2) + 4 * i + (m & 3)) * a.Ktot + 8 * (lane >> 4);
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) wf[t][kk][i] = *reinterpret_cast<const eltx8*>(wr + t * 64 + 32 * kk);
+    }
+  }
+  f32x4 bv[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int co = 32 * wm + 8 * (lane >> 4) + 4 * i;
+    bv[i] = co < a.Cout ? *reinterpret_cast<const f32x4*>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bool exact = a.Cout == 128;  // then every tile stores FN times per wave
+  elt_t* __restrict__ Y = reinterpret_cast<elt_t*>(a.y) + a.out_coff;
+
+  for (int tile = tb; tile < te; ++tile) {
+    const int b = (tile - tb) & 1;
+    if (tile > tb && exact) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FN) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // this tile's halo landed; every wave is done with the other buffer
+    if (tile + 1 < te) issue_h(tile + 1, b ^ 1);
+    const char* halo = smem + b * HBUF;
+    // the fragment addresses are rebuilt per tile from two opaque values: hoisted out of the
+    // tile loop they would take 72 VGPRs next to the 144 of weights
+    int h0 = 2 * wn * FN * HC + (lane & 15), g = lane >> 4;
+    asm volatile("" : "+v"(h0), "+v"(g));
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = bv[i];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t - 3 * ky;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int lc = kk * 4 + g;
+        eltx8 bfr[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int h = h0 + (2 * j + ky) * HC + (kx & 1) * HEVEN + (kx >> 1);
+          bfr[j] = *reinterpret_cast<const eltx8*>(halo + h * 128 + ((lc ^ (h & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = YCX_MFMA16(wf[t][kk][i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    const int n = tile / tpi, ti = tile - n * tpi;
+    const int oy0 = (ti / tx_n) * TH, ox0 = (ti % tx_n) * TW;
+    const int co = 32 * wm + 8 * (lane >> 4);
+    if (co < a.Cout) {  // cout % 8 == 0: the 8 channels are all valid
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int p = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0 + (lane & 15);
+        eltx8 ov;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const f32x4 x = act4_t<ACT>(acc[i][j], a.slope, nl2e);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)x[q];
+        }
+        if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov;
+      }
+    }
+  }
+}
+
 // TH x TW output tiles. TW = 16: a fragment is one tile row. Band mode (TW != 16, r03): TW is
 // the map's full width (40 at the 40^2 layers), so a tile is TH whole rows whose pixels are
 // consecutive in NHWC; fragment f covers band pixels 16 f .. +15, each lane finds its own
@@ -3086,6 +3215,7 @@ const TileInfo kTiles[] = {
     {256, 256, 32, "big_co256_px256_k32_s4_dma_after_mfma"},
     {64, 320, 64, "halo3x3_band_co64_8x40_s2"},
     {128, 160, 64, "halo3x3_band_co128_4x40_s2"},
+    {128, 128, 64, "halo3x3s2_wsr_co128"},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -3114,6 +3244,25 @@ ycx_status launch_ws64(ConvArgs a, hipStream_t st) {
     case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_SILU>), g, b, 0, st, a); break;
     case YCX_ACT_LEAKY: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_LEAKY>), g, b, 0, st, a); break;
     default: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_NONE>), g, b, 0, st, a); break;
+  }
+  return ycx_launch_status();
+}
+
+bool s2wsr_ok(const ConvArgs& a) {
+  return a.KH == 3 && a.KW == 3 && a.S == 2 && a.P == 1 && a.Ho % 4 == 0 && a.Wo % 16 == 0 && a.Cin == 64 &&
+         a.Cout_pad == 128 && a.out_layout == YCX_OUT_NHWC && !a.res && !a.pool &&
+         (long long)a.N * a.H * a.W * a.in_cs * 2 < (1LL << 31) - 64;
+}
+
+// tile 50: one persistent block per CU
+ycx_status launch_s2wsr(ConvArgs a, hipStream_t st) {
+  if (!s2wsr_ok(a)) return YCX_ERR_UNSUPPORTED;
+  const long long ntiles = (long long)a.N * (a.Ho / 4) * (a.Wo / 16);
+  const dim3 g((unsigned)std::min<long long>(ntiles, 256)), b(512);
+  switch (a.act) {
+    case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_SILU, 4>), g, b, 0, st, a); break;
+    case YCX_ACT_LEAKY: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_LEAKY, 4>), g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_NONE, 4>), g, b, 0, st, a); break;
   }
   return ycx_launch_status();
 }
@@ -3391,6 +3540,17 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
     if (d->cout_pad % 128 == 0) return 20;
     if (d->cout_pad == 64 && d->ho >= 160) return 19;
   }
+  // 3x3/s2 64 -> 128 downsample with >= 4 output tiles per persistent block: weights in
+  // registers, input halo in LDS (tile 50; YCX_NO_S2WSR=1 keeps the im2col tiles for A/B)
+  if (allow_wres && d->kh == 3 && d->kw == 3 && d->stride == 2 && d->pad == 1 && d->cin == 64 &&
+      d->cout_pad == 128 && d->out_layout == YCX_OUT_NHWC && d->ho % 4 == 0 && d->wo % 16 == 0 &&
+      (long long)d->n * (d->ho / 4) * (d->wo / 16) >= 2048) {
+    static const bool off = [] {
+      const char* e = getenv("YCX_NO_S2WSR");
+      return e && atoi(e) != 0;
+    }();
+    if (!off) return 50;
+  }
   // 40-wide maps (not 16-aligned): the 8 x 40 band halo tile where it has >= 2.5 waves of
   // workgroups (40^2 bs 32 256->512: 0.113 vs 0.124 ms; with fewer workgroups it loses to tile 16,
   // profiles/r03/band_halo_40.txt)
@@ -3532,6 +3692,7 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x,
     case 47: return launch_bigt<256, 256, 4, 4, 4, 3>(a, st);  // tile 40 likewise
     case 48: return launch_halo<64, 2, 4, 2, 8, 40>(a, st);      // band halo tiles (40-wide maps)
     case 49: return launch_halo<128, 4, 2, 2, 4, 40>(a, st);
+    case 50: return launch_s2wsr(a, st);
 #ifdef YCX_EXPERIMENTAL_TILES  // retired experiments (tools/build_variant.sh NAME -DYCX_EXPERIMENTAL_TILES)
     case 27: return launch_p8<256, 256>(a, st);
     case 28: return launch_p8<128, 256>(a, st);
