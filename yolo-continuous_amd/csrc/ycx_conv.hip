@@ -1929,19 +1929,35 @@ __global__ void __launch_bounds__(512) conv3x3_ws64(ConvArgs a) {
 // Requires Cin == 64, Cout_pad == 128, pad 1, Ho % TH == Wo % 16 == 0, NHWC output
 // without residual.
 // -------------------------------------------------------------------------
-template <int ACT, int TH>
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the largest case <= n; I is the cap)
+template <int I>
+__device__ __forceinline__ void vm_wait_le(int n) {
+  if constexpr (I > 0) {
+    if (n >= I) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(I) : "memory");
+      return;
+    }
+    vm_wait_le<I - 1>(n);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+template <int ACT, int TH, int NB>
 __global__ void __launch_bounds__(512) conv3x3s2_wsr(ConvArgs a) {
   constexpr int NW = 8, TW = 16, HC = 2 * TW + 1, HP = (2 * TH + 1) * HC;  // 17 x 33 halo pixels
   constexpr int HEVEN = TW + 1;                                                   // even columns: slots 0..16
   constexpr int HPIECES = (HP + 7) / 8, HPW = (HPIECES + NW - 1) / NW;           // 1-KB DMA pieces (8 pixels)
   constexpr int HBUF = HPIECES * 1024;
   constexpr int FM = 2, FN = TH / 2;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * HBUF];
+  static_assert(NB >= 2 && NB * HBUF <= 160 * 1024, "halo ring in LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[NB * HBUF];
   const float nl2e = silu_nl2e();
   const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
   const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
+  const int nh = (HPIECES - wid + NW - 1) / NW;  // this wave's halo DMAs per tile
   const int lrow = lane >> 3, pch = lane & 7;
   const int tx_n = a.Wo / TW, tpi = (a.Ho / TH) * tx_n, ntiles = a.N * tpi;
   const int blk = ycx_xcd_remap(blockIdx.x, gridDim.x);
@@ -1986,13 +2002,17 @@ __global__ void __launch_bounds__(512) conv3x3s2_wsr(ConvArgs a) {
   }
   const bool exact = a.Cout == 128;  // then every tile stores FN times per wave
   elt_t* __restrict__ Y = reinterpret_cast<elt_t*>(a.y) + a.out_coff;
+  for (int q = 1; q < NB - 1; ++q)
+    if (tb + q < te) issue_h(tb + q, q);
 
   for (int tile = tb; tile < te; ++tile) {
-    const int b = (tile - tb) & 1;
-    if (tile > tb && exact) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FN) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // this tile's halo landed; every wave is done with the other buffer
-    if (tile + 1 < te) issue_h(tile + 1, b ^ 1);
+    const int k = tile - tb, b = k % NB;
+    // in flight behind this tile's halo: the halos of the next min(NB - 2, te - 1 - tile) tiles,
+    // then (exact, k > 0) the previous tile's FN stores; the weights came before them
+    const int ahead = min(NB - 2, te - 1 - tile);
+    vm_wait_le<(NB - 2) * HPW + FN>(ahead * nh + (k > 0 && exact ? FN : 0));
+    __syncthreads();  // this tile's halo landed; every wave is done with the previous tile's buffer
+    if (tile + NB - 1 < te) issue_h(tile + NB - 1, (k + NB - 1) % NB);
     const char* halo = smem + b * HBUF;
     // the fragment addresses are rebuilt per tile from two opaque values: hoisted out of the
     // tile loop they would take 72 VGPRs next to the 144 of weights
@@ -3254,15 +3274,18 @@ bool s2wsr_ok(const ConvArgs& a) {
          (long long)a.N * a.H * a.W * a.in_cs * 2 < (1LL << 31) - 64;
 }
 
-// tile 50: one persistent block per CU
+// tile 50: one persistent block per CU; NB halo buffers (NB - 1 tiles in flight)
+#ifndef YCX_S2WSR_NB
+#define YCX_S2WSR_NB 2
+#endif
 ycx_status launch_s2wsr(ConvArgs a, hipStream_t st) {
   if (!s2wsr_ok(a)) return YCX_ERR_UNSUPPORTED;
   const long long ntiles = (long long)a.N * (a.Ho / 4) * (a.Wo / 16);
   const dim3 g((unsigned)std::min<long long>(ntiles, 256)), b(512);
   switch (a.act) {
-    case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_SILU, 4>), g, b, 0, st, a); break;
-    case YCX_ACT_LEAKY: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_LEAKY, 4>), g, b, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_NONE, 4>), g, b, 0, st, a); break;
+    case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_SILU, 4, YCX_S2WSR_NB>), g, b, 0, st, a); break;
+    case YCX_ACT_LEAKY: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_LEAKY, 4, YCX_S2WSR_NB>), g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_NONE, 4, YCX_S2WSR_NB>), g, b, 0, st, a); break;
   }
   return ycx_launch_status();
 }
