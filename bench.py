@@ -411,20 +411,45 @@ def image_in_leg(args, det, dev, dist_on, gather):
                          f"inside the step; {args.image_in_steps} timed steps")
 
 
+def visible_gpus(env=None, kfd_nodes="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs a child process may use, found WITHOUT any HIP / torch.cuda call (the
+    launcher parent must never initialise the GPU runtime): the shortest of the
+    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES lists when
+    one is set, else the KFD topology nodes with SIMDs (CPU nodes have none);
+    None when neither is readable (each rank then checks LOCAL_RANK itself)."""
+    env = os.environ if env is None else env
+    lists = [env[k] for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES") if k in env]
+    if lists:
+        return min(len([t for t in v.split(",") if t.strip()]) for v in lists)
+    try:
+        nodes = os.listdir(kfd_nodes)
+    except OSError:
+        return None
+    n = 0
+    for d in nodes:
+        try:
+            with open(os.path.join(kfd_nodes, d, "properties")) as f:
+                props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    return n
+
+
 def launch_ranks(args, argv):
     """``--gpus N`` (N > 1) without WORLD_SIZE in the environment: start N rank
     processes of this same script, one per GPU (RANK = LOCAL_RANK = i,
     WORLD_SIZE = N, rendezvous on 127.0.0.1 at a free port), and return the
-    worst exit code. The parent never touches the GPU (it only counts devices,
-    which does not initialise HIP on this image) and starts the ranks as child
-    processes, never by exec. If a rank fails the others are stopped instead
+    worst exit code. The parent never touches the GPU (visible_gpus reads the
+    environment / sysfs, no HIP or torch.cuda call) and starts the ranks as
+    child processes, never by exec. If a rank fails the others are stopped instead
     of waiting at a barrier forever."""
     import socket
     import subprocess
-    if not args.dry_run:
-        have = torch.cuda.device_count()
-        if have < args.gpus:
-            raise SystemExit(f"--gpus {args.gpus} but only {have} GPU(s) are visible")
+    have = None if args.dry_run else visible_gpus()  # the dry run uses no GPU
+    if have is not None and have < args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but only {have} GPU(s) are visible")
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -501,6 +526,8 @@ def main(argv=None):
     if args.dry_run:
         return dry_run(args, world, rank)
     rnd = args.round or _current_round()
+    if local >= torch.cuda.device_count():  # the launcher could not count devices: the rank checks its own
+        raise SystemExit(f"LOCAL_RANK {local} but only {torch.cuda.device_count()} GPU(s) are visible")
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     dist_on = world > 1 or args.dist  # --dist: the N > 1 code path (RCCL gather) on a single rank

@@ -325,9 +325,11 @@ ycx_status ycx_correct_boxes(const ycx_correct_desc* d, float* dets, const int32
 ycx_status ycx_run_ops(const ycx_op* ops, int32_t n_ops, void* stream, void* const* events);
 
 /* 1: ycx_run_ops wraps every op in a roctx range "op<i> <kind> <tile> n HxW cin->cout k s"
- * (rocprofv3 --marker-trace); 0 (default): no tracing. No reference counterpart
- * (its only instrument is the @timer decorator, utils/helper_torch.py:10-20). */
-void ycx_set_trace(int32_t on);
+ * (rocprofv3 --marker-trace); 0 (default): no tracing. The roctx library is dlopen'ed
+ * on the first ycx_set_trace(1); YCX_ERR_UNSUPPORTED (tracing stays off) if it is
+ * absent. No reference counterpart (its only instrument is the @timer decorator,
+ * utils/helper_torch.py:10-20). */
+ycx_status ycx_set_trace(int32_t on);
 /* Kernel-side bounds checks (`make -C yolo-continuous_amd/csrc debug` builds
  * libycx_hip_dbg.so with -DYCX_DEBUG_BOUNDS; select it with YCX_LIB=<path>): every
  * conv epilogue store is tested against the output extent its descriptor implies and

@@ -115,7 +115,9 @@ int main(void) {
   uint32_t oob[2] = {7, 7};
   EXPECT(ycx_debug_bounds(oob, 0) == YCX_ERR_UNSUPPORTED && oob[0] == 0); /* release build */
   EXPECT(ycx_debug_bounds(NULL, 0) == YCX_ERR_BAD_ARG);
-  ycx_set_trace(0);
+  EXPECT(ycx_set_trace(0) == YCX_OK);
+  EXPECT(ycx_set_trace(1) == YCX_OK); /* roctx resolved at run time (dlopen), not at link time */
+  EXPECT(ycx_set_trace(0) == YCX_OK);
 
   if (fails) {
     fprintf(stderr, "abi_check: %d failures\n", fails);

@@ -126,3 +126,47 @@ def test_bench_launches_n_ranks_itself():
     out = json.loads(lines[0])
     assert out["rccl_world_size"] == 2 and out["n_gpus"] == 2 and out["rank_major_order"]
     assert out["gathered_dets"] == [8, 300, 7] and out["gathered_keep"] == [8, 300]
+
+
+def test_launcher_parent_never_initialises_the_gpu(tmp_path):
+    """the rank launcher counts GPUs from the environment /
+    KFD sysfs only. In a child interpreter every torch.cuda entry that could
+    reach HIP is made to raise; the 2-rank dry run must still succeed, leave
+    torch.cuda uninitialised in the parent, and refuse --gpus 2 when only one
+    device is visible."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prog = f"""
+import sys, torch
+sys.path.insert(0, {repo!r})
+def boom(*a, **k):
+    raise AssertionError("launcher parent touched torch.cuda")
+for name in ("device_count", "init", "_lazy_init", "is_available", "set_device", "synchronize"):
+    setattr(torch.cuda, name, boom)
+import bench
+rc = bench.main(["--gpus", "2", "--dry-run", "--batch", "2"])
+assert not torch.cuda.is_initialized()
+print("RC", rc)
+"""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["HIP_VISIBLE_DEVICES"] = "0,1"
+    r = subprocess.run([sys.executable, "-c", prog], env=env, capture_output=True, text=True, timeout=180, cwd=repo)
+    assert r.returncode == 0 and "RC 0" in r.stdout, r.stderr[-2000:]
+    env["HIP_VISIBLE_DEVICES"] = "0"  # the real (non-dry) launcher refuses before it starts any rank
+    prog = prog.replace('"--dry-run", ', "")
+    r = subprocess.run([sys.executable, "-c", prog], env=env, capture_output=True, text=True, timeout=180, cwd=repo)
+    assert r.returncode != 0 and "only 1 GPU(s) are visible" in r.stderr
+
+
+def test_visible_gpus_from_kfd_topology(tmp_path):
+    """visible_gpus without *_VISIBLE_DEVICES: KFD nodes with SIMDs are GPUs."""
+    import bench
+    for i, simds in enumerate((0, 1024, 1024, 0)):
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 8\nsimd_count {simds}\n")
+    assert bench.visible_gpus(env={}, kfd_nodes=str(tmp_path)) == 2
+    assert bench.visible_gpus(env={}, kfd_nodes=str(tmp_path / "missing")) is None
+    assert bench.visible_gpus(env={"ROCR_VISIBLE_DEVICES": "0,1,2", "HIP_VISIBLE_DEVICES": "1"}) == 1

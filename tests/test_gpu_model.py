@@ -265,3 +265,32 @@ def test_chunked_prefix_bit_identical(device, precision, monkeypatch):
         assert torch.equal(a, b)
     assert torch.equal(c0, c1) and torch.equal(k0, k1) and torch.equal(d0, d1)
     det.close()
+
+
+def test_concurrent_detector_dropped_in_flight(device):
+    """a ConcurrentDetector dropped (no close()) right after submit():
+    its slot engines are released by their finalisers while the batches may still
+    run on the slot streams. The release waits for the device first, so memory
+    handed back to the caching allocator and then overwritten cannot corrupt the
+    detections still referenced by the caller."""
+    import gc
+    from ycx.detect import ConcurrentDetector, Detector
+    mask = [[6, 7, 8], [3, 4, 5], [0, 1, 2]]
+    m, _ = make_model('yolov7', 80, 0, 'bf16')
+    m.to(device)
+    shape = (4, 3, 160, 160)
+    x = synthetic_images(*shape, seed=7).to(device)
+    ref = Detector(m, shape, device, ANCHORS, mask, conf_thres=0.3, nms_thres=0.45, max_det=500)
+    d_ref, k_ref, c_ref = [t.clone() for t in ref(x)]
+    ref.close()
+    base = len(m._engines)
+    cd = ConcurrentDetector(m, shape, device, ANCHORS, mask, depth=3, conf_thres=0.3, nms_thres=0.45, max_det=500)
+    outs = [cd.submit(x)[:3] for _ in range(3)]
+    del cd
+    gc.collect()
+    assert len(m._engines) == base
+    junk = torch.full((64 << 20,), 7, dtype=torch.int32, device=device)  # reuses the released blocks
+    torch.cuda.synchronize()
+    del junk
+    for d, k, c in outs:
+        assert torch.equal(c, c_ref) and torch.equal(k, k_ref) and torch.equal(d, d_ref)

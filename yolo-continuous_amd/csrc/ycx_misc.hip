@@ -8,9 +8,9 @@
 // Each thread moves one 16-byte vector (8 bf16 or 4 fp32 channels); consecutive
 // threads take consecutive channel chunks of one pixel, so every wave reads and
 // writes whole contiguous channel rows.
-#include <vector>
-#include <rocprofiler-sdk-roctx/roctx.h>
+#include <dlfcn.h>
 #include <stdio.h>
+#include <vector>
 
 #include "ycx_internal.h"
 
@@ -444,9 +444,30 @@ static ycx_status run_one(const ycx_op& op, void* stream) {
 // op names its index, kind, kernel tile and shape, so a `rocprofv3 --marker-trace`
 // timeline of an eager forward lines each kernel up with its Model.forward layer.
 // (A HIP-graph replay has no host loop: trace an eager run.)
+// The roctx library is resolved with dlopen on the first ycx_set_trace(1), so the product
+// library carries no link-time dependency on the profiler SDK.
 static int g_trace = 0;
+static int (*g_roctx_push)(const char*) = nullptr;
+static int (*g_roctx_pop)() = nullptr;
 
-extern "C" void ycx_set_trace(int32_t on) { g_trace = on != 0; }
+extern "C" ycx_status ycx_set_trace(int32_t on) {
+  if (!on) {
+    g_trace = 0;
+    return YCX_OK;
+  }
+  if (!g_roctx_push) {
+    void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librocprofiler-sdk-roctx.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return YCX_ERR_UNSUPPORTED;
+    auto push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+    auto pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+    if (!push || !pop) return YCX_ERR_UNSUPPORTED;
+    g_roctx_pop = pop;
+    g_roctx_push = push;
+  }
+  g_trace = 1;
+  return YCX_OK;
+}
 
 static void trace_push(int32_t i, const ycx_op& op) {
   static const char* kinds[] = {"?", "conv", "stem", "pool", "copy", "stem2", "head"};
@@ -460,7 +481,7 @@ static void trace_push(int32_t i, const ycx_op& op) {
   } else {
     snprintf(buf, sizeof buf, "op%d %s", i, k);
   }
-  roctxRangePushA(buf);
+  g_roctx_push(buf);
 }
 
 extern "C" ycx_status ycx_run_ops(const ycx_op* ops, int32_t n_ops, void* stream, void* const* events) {
@@ -471,7 +492,7 @@ extern "C" ycx_status ycx_run_ops(const ycx_op* ops, int32_t n_ops, void* stream
       return YCX_ERR_LAUNCH;
     if (g_trace) trace_push(i, ops[i]);
     ycx_status s = run_one(ops[i], stream);
-    if (g_trace) roctxRangePop();
+    if (g_trace) g_roctx_pop();
     if (s != YCX_OK) return s;
   }
   if (events && hipEventRecord(reinterpret_cast<hipEvent_t>(events[n_ops]), st) != hipSuccess)

@@ -140,7 +140,7 @@ _SIGS = [
     ("ycx_nms_workspace_size", ctypes.c_size_t, [ctypes.POINTER(NmsDesc)]),
     ("ycx_sort_nms", _i32, [ctypes.POINTER(NmsDesc), _VP, _VP, _VP, _VP, ctypes.c_size_t, _VP, _VP, _VP, _VP]),
     ("ycx_run_ops", _i32, [ctypes.POINTER(Op), _i32, _VP, ctypes.POINTER(_VP)]),
-    ("ycx_set_trace", None, [_i32]),
+    ("ycx_set_trace", _i32, [_i32]),
     ("ycx_debug_bounds", _i32, [ctypes.POINTER(ctypes.c_uint32), _i32]),
     ("ycx_graph_capture", _i32, [ctypes.POINTER(Op), _i32, _VP, ctypes.POINTER(_VP)]),
     ("ycx_graph_launch", _i32, [_VP, _VP]),
@@ -181,7 +181,10 @@ lib = _load()
 # YCX_ROCTX=1: one roctx range per op of every eager ycx_run_ops (rocprofv3 --marker-trace);
 # Detector then runs eagerly, since a HIP-graph replay has no host loop to mark
 TRACE = bool(os.environ.get("YCX_ROCTX"))
-lib.ycx_set_trace(1 if TRACE else 0)
+if TRACE and lib.ycx_set_trace(1) != 0:
+    import warnings
+    warnings.warn("ycx: YCX_ROCTX set but librocprofiler-sdk-roctx could not be loaded; tracing is off")
+    TRACE = False
 
 
 def check(status: int, what: str = "") -> None:

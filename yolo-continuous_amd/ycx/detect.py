@@ -270,9 +270,19 @@ class DevicePost:
 
 
 def _release_engine(model_ref, shape, device, slot):
+    """Drop a private engine (activations, packed weights, HIP graph). Its
+    kernels may still run on a slot stream that the caching allocator does not
+    know about (the engine's buffers carry no record_stream), and the graph may
+    still be executing: wait for the whole device first, so neither the memory
+    nor the graph is reused or destroyed under work in flight."""
     model = model_ref()
-    if model is not None:
-        model.release_slot(shape, device, slot)
+    if model is None:
+        return
+    try:
+        torch.cuda.synchronize(torch.device(device))
+    except RuntimeError:  # interpreter shutdown: the runtime is already gone, nothing can still run
+        pass
+    model.release_slot(shape, device, slot)
 
 
 class Detector:
@@ -327,7 +337,7 @@ class Detector:
 
     def close(self):
         """Release this Detector's private engine (activations, packed weights,
-        HIP graph). Work already queued on its buffers must have completed; the
+        HIP graph) once the device has finished the work queued on it; the
         Detector is unusable afterwards."""
         if self._release is not None:
             self._release()
