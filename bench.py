@@ -36,6 +36,7 @@ ANCHORS = [[12, 16, 19, 36, 40, 28], [36, 75, 76, 55, 72, 146], [142, 110, 192, 
 MASK = [[6, 7, 8], [3, 4, 5], [0, 1, 2]]
 METRIC = "images/sec (whole node) + p50 end-to-end latency, 640×640 bs=32, 1/2/4/8 MI355X"
 PEAK = {"bf16": 2500.0, "fp16": 2500.0, "f32": 157.3, "fp8": 5000.0}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # HBM3E peak (MI355X_MICROARCH.md)
 
 
 def _current_round():
@@ -106,6 +107,29 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def op_gap_table(op_info, per_op_ms, peak_tflops, hbm_gbs=HBM_PEAK_GBS):
+    """One row per plan op: its algorithmic FLOPs and HBM bytes (engine op_info:
+    input once, weights once, residual once, output once), the bound it sits
+    under (MFMA when FLOP / peak exceeds bytes / HBM peak, i.e. above the
+    peak / HBM ridge, 312 FLOP/B for bf16), the floor time that bound implies,
+    the achieved fraction of it (floor / measured) and the gap in ms."""
+    rows = []
+    for i, info in enumerate(op_info):
+        ms = per_op_ms[i]
+        fl, by = int(info.get('flops', 0)), int(info.get('bytes', 0))
+        t_mfma = fl / (peak_tflops * 1e12) * 1e3
+        t_hbm = by / (hbm_gbs * 1e9) * 1e3
+        floor = max(t_mfma, t_hbm)
+        rows.append(dict(i=i, name=info['name'], kind=info.get('kind'), shape=info.get('shape'), ms=round(ms, 5),
+                         flops=fl, bytes=by, bound='mfma' if t_mfma > t_hbm else 'hbm',
+                         intensity=round(fl / by, 1) if by else None,
+                         floor_ms=round(floor, 5), frac=round(floor / ms, 4) if ms > 0 else None,
+                         gap_ms=round(max(0.0, ms - floor), 5),
+                         tflops=round(fl / (ms * 1e-3) / 1e12, 1) if fl and ms > 0 else None,
+                         gbs=round(by / (ms * 1e-3) / 1e9, 1) if by and ms > 0 else None))
+    return rows
+
+
 def roofline(det, steps, precision):
     """Per-op HIP events around every op of the plan (recorded on the plan's
     stream by ycx_run_ops) for `steps` extra forwards; returns the dominant
@@ -140,10 +164,25 @@ def roofline(det, steps, precision):
     all_conv_ms = sum(v['ms'] for v in per.values() if v['flops'] > 0)
     all_conv_tf = sum(v['flops'] for v in per.values()) / (all_conv_ms * 1e-3) / 1e12
     fwd_ms = sum(v['ms'] for v in per.values())
-    ops = [dict(i=i, name=info['name'], ms=round(per_op[i], 5), shape=info.get('shape'),
-                tflops=round(info['flops'] / (per_op[i] * 1e-3) / 1e12, 1) if info.get('flops') else None)
-           for i, info in enumerate(eng.op_info)]
+    ops = op_gap_table(eng.op_info, per_op, PEAK[precision])
+    # the dominant kernel's launches split by the bound each one sits under (its frac above mixes them)
+    split = {}
+    for o in ops:
+        if o['name'] == dom:
+            s = split.setdefault(o['bound'], dict(launches=0, ms=0.0, flops=0, bytes=0, floor_ms=0.0))
+            s['launches'] += 1
+            s['ms'] += o['ms']
+            s['flops'] += o['flops']
+            s['bytes'] += o['bytes']
+            s['floor_ms'] += o['floor_ms']
+    for b, s in split.items():
+        s['frac_of_bound'] = round(s['floor_ms'] / s['ms'], 4) if s['ms'] else None
+        s['tflops'] = round(s['flops'] / (s['ms'] * 1e-3) / 1e12, 1) if s['ms'] else None
+        s['ms'] = round(s['ms'], 5)
+        s['floor_ms'] = round(s['floor_ms'], 5)
     return dict(kernel=dom, avg_launch_ms=avg_ms, ops=ops, flops_per_launch=flops_per_launch, achieved=achieved,
+                dominant_by_bound=split, forward_floor_ms=sum(o['floor_ms'] for o in ops),
+                forward_gap_ms=sum(o['gap_ms'] for o in ops),
                 all_conv_tflops=all_conv_tf, all_conv_ms=all_conv_ms, forward_kernel_ms=fwd_ms,
                 per_kernel={k: dict(ms=round(v['ms'], 4), launches=v['launches'],
                                     tflops=(round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1) if v['flops'] else None))
@@ -590,6 +629,7 @@ def main(argv=None):
     if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    det.check()  # outside the timed region: no batch left the plan's range (fp16: |a| <= 65504)
     lat = [a.elapsed_time(b) for a, b in lat_ev]
     # unloaded latency: one batch in flight at a time (input resident -> detections, + gather)
     lat1 = []
@@ -642,16 +682,24 @@ def main(argv=None):
                          "avg_launch_ms": round(rl['avg_launch_ms'], 5),
                          "flops_per_launch": int(rl['flops_per_launch']),
                          "all_conv_tflops": round(rl['all_conv_tflops'], 2),
-                         "forward_kernel_ms": round(rl['forward_kernel_ms'], 4)},
+                         "forward_kernel_ms": round(rl['forward_kernel_ms'], 4),
+                         "forward_floor_ms": round(rl['forward_floor_ms'], 4),
+                         "forward_gap_ms": round(rl['forward_gap_ms'], 4),
+                         "dominant_by_bound": rl['dominant_by_bound'],
+                         "top_gaps": [[o['i'], o['name'], o['bound'], o['ms'], o['floor_ms'], o['gap_ms']]
+                                      for o in sorted(rl['ops'], key=lambda o: -o['gap_ms'])[:8]]},
             "cpu_baseline": cpu,
             "rccl_world_size": dist.get_world_size() if dist_on else 1,
             **(img_in or {}),
             "detections_last_step": int(kc.sum().item()),
         }
         print(json.dumps(out), flush=True)
-        if os.environ.get("YCX_BENCH_KERNELS"):
+        if os.environ.get("YCX_BENCH_KERNELS"):  # the per-op roofline gap table (serial leg, HIP events)
             with open(os.environ["YCX_BENCH_KERNELS"], "w") as f:
-                json.dump(dict(per_kernel=rl['per_kernel'], ops=rl['ops']), f, indent=1)
+                json.dump(dict(precision=args.precision, shape=list(shape), peak_tflops=peak,
+                               hbm_peak_gbs=HBM_PEAK_GBS, forward_kernel_ms=rl['forward_kernel_ms'],
+                               forward_floor_ms=rl['forward_floor_ms'], forward_gap_ms=rl['forward_gap_ms'],
+                               per_kernel=rl['per_kernel'], ops=rl['ops']), f, indent=1)
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()

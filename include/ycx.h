@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define YCX_ABI_VERSION 7
+#define YCX_ABI_VERSION 8
 
 typedef int32_t ycx_status;
 enum {
@@ -224,6 +224,7 @@ typedef struct ycx_op {
   void* cand;               /* HEAD: ycx_cand [n][rows_total]                      */
   int32_t* cand_rows;       /* HEAD: [n][rows_total]                                */
   int32_t* cand_counts;     /* HEAD: [n], zeroed before the first level's op        */
+  int32_t* status;          /* HEAD (nullable): the range guard flag, below         */
 } ycx_op;
 
 int ycx_abi_version(void);
@@ -250,10 +251,16 @@ ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const void* w,
  * out_layout YCX_OUT_NCHW_F32) fused with that level's decode + filter: appends
  * the passing rows to cand / cand_rows / cand_counts exactly as
  * ycx_decode_filter does. `heads` (nullable) also receives the raw fp32 NCHW
- * logits [n][cout][ho][wo] (the compat Model.forward output). */
+ * logits [n][cout][ho][wo] (the compat Model.forward output).
+ * `status` (nullable, one int32 the caller zeroes): set to YCX_HEAD_NONFINITE when
+ * any logit of the launch is inf or NaN -- the fp16 plan's range guard (an
+ * activation past 65504 becomes inf at its producer's store and reaches the heads
+ * as inf / NaN). Never cleared by the library. No reference counterpart: the
+ * reference computes in fp32 (nets/yolo.py:143-153). */
+enum { YCX_HEAD_NONFINITE = 1 };
 ycx_status ycx_conv2d_head(const ycx_conv_desc* d, const ycx_head_desc* h, const void* x, const void* w,
                            const float* bias, float* heads, ycx_cand* cand, int32_t* cand_rows,
-                           int32_t* cand_counts, void* stream);
+                           int32_t* cand_counts, int32_t* status, void* stream);
 /* Stem conv: fp32 NCHW input (the model input, cin <= 4), weights fp32
  * [kh][kw][cin][cout_pad], output NHWC in d->dtype. in_c_* describe the NCHW
  * channel count (in_c_stride = channels of the input tensor). */

@@ -166,3 +166,78 @@ def fused_keep_report(cand, cand_rows, counts, keep, kc, b, heads_b, nc, conf, i
                 member_max_dist=max(boundary) if boundary else 0.0, box_maxdiff=box_maxdiff, cls_same=cls_same,
                 nms_exact=bool(nms_exact), n_keep=k, n_keep_ref=len(ref_rows), keep_flips=keep_flips,
                 unexplained_flips=unexplained)
+
+
+def decoded_flip_report(dec_dev, dec_ref, nc, conf, iou):
+    """Attribute every difference between the oracle's greedy chain (filter +
+    per-class NMS, detect.py:98-137) run on two decoded tensors of ONE image --
+    ``dec_dev`` from the device's forward, ``dec_ref`` from the oracle's -- to
+    the forward's perturbation of scores and boxes:
+
+      - ``member_flips``: rows that pass conf_thres on one side only; each must
+        lie within ``max_score_delta`` of the threshold (``member_far`` counts
+        those that do not);
+      - keep flips: in every class with a differing keep decision, the flip
+        that comes first in the oracle's greedy order must be caused directly:
+        a membership flip at or above it, a score-order swap at or above it, or
+        a kept higher-ranked box whose fp32 IoU with it lies on different sides
+        of nms_thres under the two box sets (``unexplained_flips`` counts the
+        classes where none holds; later flips of a class cascade from the
+        first).
+    Rows are compared by index, so both tensors must be (rows, 5 + nc) xywh."""
+    from oracle import ref_post
+
+    def prep(d):
+        d = d.detach().to('cpu', torch.float32).clone()
+        xyxy = torch.stack([d[:, 0] - d[:, 2] / 2, d[:, 1] - d[:, 3] / 2,
+                            d[:, 0] + d[:, 2] / 2, d[:, 1] + d[:, 3] / 2], 1)
+        cc, ci = torch.max(d[:, 5:5 + nc], 1)
+        return xyxy.numpy(), (d[:, 4] * cc).numpy(), ci.numpy()
+
+    bd, sd_, cd = prep(dec_dev)
+    br, sr, cr = prep(dec_ref)
+    kd = ref_post.nms_keep_rows(dec_dev.detach().to('cpu', torch.float32).clone().unsqueeze(0), nc, conf, iou)[0][0]
+    kr = ref_post.nms_keep_rows(dec_ref.detach().to('cpu', torch.float32).clone().unsqueeze(0), nc, conf, iou)[0][0]
+    kd, kr = set(kd.tolist()), set(kr.tolist())
+    pd_, pr = set(np.flatnonzero(sd_ >= conf).tolist()), set(np.flatnonzero(sr >= conf).tolist())
+    member = pd_ ^ pr
+    union = sorted(pd_ | pr)
+    delta = float(np.abs(sd_[union] - sr[union]).max()) if union else 0.0
+    member_far = sum(1 for r in member if abs(float(sr[r]) - conf) > delta)
+    cls_flips = sum(1 for r in union if cd[r] != cr[r])
+    flipped = kd ^ kr
+
+    def iou_gt(b, i, js):
+        a = b[js].astype(np.float32).reshape(-1, 4)
+        f = b[i].astype(np.float32)
+        with np.errstate(invalid='ignore', divide='ignore'):
+            w = np.maximum(np.float32(0), np.minimum(a[:, 2], f[2]) - np.maximum(a[:, 0], f[0]))
+            h = np.maximum(np.float32(0), np.minimum(a[:, 3], f[3]) - np.maximum(a[:, 1], f[1]))
+            inter = w * h
+            den = (a[:, 2] - a[:, 0]) * (a[:, 3] - a[:, 1]) + (f[2] - f[0]) * (f[3] - f[1]) - inter
+            return (inter / den).astype(np.float64) > iou
+
+    unexplained, classes = 0, 0
+    for k in sorted({int(cr[r]) for r in flipped} | {int(cd[r]) for r in flipped}):
+        members = [r for r in union if int(cr[r]) == k or int(cd[r]) == k]
+        cand_f = [r for r in flipped if r in members]
+        if not cand_f:
+            continue
+        classes += 1
+        order_r = sorted(members, key=lambda r: (-float(sr[r]), r))
+        order_d = sorted(members, key=lambda r: (-float(sd_[r]), r))
+        rank = {r: i for i, r in enumerate(order_r)}
+        first = min(cand_f, key=lambda r: rank[r])
+        pos = rank[first]
+        above = order_r[:pos]
+        if any(r in member or cd[r] != cr[r] for r in above + [first]):
+            continue  # a membership / class flip at or above it changes the greedy input
+        if order_d[:pos + 1] != order_r[:pos + 1]:
+            continue  # a score-order swap at or above it
+        higher = [r for r in above if r in kr]  # kept by both chains (all decisions above agree)
+        if higher and bool(np.any(iou_gt(bd, first, higher) != iou_gt(br, first, higher))):
+            continue  # an IoU threshold crossing against a kept higher-ranked box
+        unexplained += 1
+    return dict(n_pass_dev=len(pd_), n_pass_ref=len(pr), member_flips=len(member), member_far=member_far,
+                max_score_delta=delta, cls_flips=cls_flips, n_keep_dev=len(kd), n_keep_ref=len(kr),
+                keep_flips=len(flipped), flip_classes=classes, unexplained_flips=unexplained)

@@ -27,7 +27,7 @@ def main():
     for p in args.libs:
         lib = ctypes.CDLL(os.path.abspath(p))
         lib.ycx_conv2d_head.restype = ctypes.c_int32
-        lib.ycx_conv2d_head.argtypes = [ctypes.c_void_p] * 10
+        lib.ycx_conv2d_head.argtypes = [ctypes.c_void_p] * 11
         libs.append(lib)
     dev = torch.device("cuda:0")
     st = L.stream_handle(dev)
@@ -58,7 +58,7 @@ def main():
             cnt = torch.zeros((n,), dtype=torch.int32, device=dev)
             outs.append((cand, rows, cnt))
         calls = [(lib, (ctypes.byref(d), ctypes.byref(hd), x.data_ptr(), wt.data_ptr(), b.data_ptr(), None,
-                        o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(), st)) for lib, o in zip(libs, outs)]
+                        o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(), None, st)) for lib, o in zip(libs, outs)]
         times = [[] for _ in libs]
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for r in range(args.rounds):

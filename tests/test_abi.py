@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_metadata_without_gpu():
     from ycx import _lib
-    assert _lib.lib.ycx_abi_version() == _lib.ABI_VERSION == 7
+    assert _lib.lib.ycx_abi_version() == _lib.ABI_VERSION == 8
     for i, st in enumerate(_lib._STRUCTS):
         assert _lib.lib.ycx_struct_size(i) == ctypes.sizeof(st)
     assert _lib.lib.ycx_struct_size(99) == 0

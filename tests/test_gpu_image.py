@@ -6,7 +6,7 @@ import pytest
 import torch
 import yaml
 
-from helpers import ANCHORS, MASK
+from helpers import ANCHORS, MASK, rel_err
 from oracle import ref_letterbox
 from ycx.utils.target_box import TargetBox
 from ycx.detect import correct_boxes_device, predict, yolo_correct_boxes
@@ -99,8 +99,11 @@ def test_predict_vs_oracle_chain(device, tmp_path, precision, size, hw):
     default precision) at 640 on a 773x512 image, BASELINE C1's plumbing shape (also
     run in f32, strictly): the seeded weights keep ~1.9k heavily overlapping boxes of
     the one class, so a score that moves by ~1e-4 can flip a greedy decision and the
-    flips cascade; >= 97 % of the boxes must match (corners within one pixel, score
-    within 1e-3; measured r03 on MI355X: 1890 of 1934, 97.7 %)."""
+    flips cascade (r03: 44 of 1934 boxes differ). The difference is decomposed: predict's
+    boxes are exactly the device chain's rows; the oracle's NMS on the device's own decoded
+    tensor keeps exactly the device's rows; the decoded tensors are within 1e-3; and the
+    first keep flip of every class is caused by a threshold crossing, a score swap or an
+    IoU crossing under the forward's perturbation (helpers.decoded_flip_report)."""
     from oracle import ref_forward, ref_letterbox, ref_post
     from ycx.utils.helper_io import cvt_cfg
     from ycx.utils.synth import synthetic_state_dict
@@ -145,21 +148,42 @@ def test_predict_vs_oracle_chain(device, tmp_path, precision, size, hw):
                 used.add(i if i in js else js[0])
         assert not bad, (len(bad), bad[:4])
         return
-    # fp16: scores move by ~1e-4, so equal-class boxes of near-equal score may swap places and a
-    # box at a threshold may flip: match as multisets (each oracle box to an unused predicted box
-    # with corners within one pixel and score within 1e-3)
-    g = np.array([[tb.left, tb.top, tb.right, tb.bottom, float(tb.score)] for tb in got], dtype=np.float64)
-    want = np.stack([np.maximum(0, np.floor(res[:, 1])), np.maximum(0, np.floor(res[:, 0])),
-                     np.minimum(img.shape[1], np.floor(res[:, 3])), np.minimum(img.shape[0], np.floor(res[:, 2])),
-                     res[:, 4].astype(np.float64) * res[:, 5]], 1)
-    used = np.zeros(len(g), bool)
-    matched = 0
-    for w in want:
-        ok = (np.abs(g[:, :4] - w[:4]).max(1) <= 1) & (np.abs(g[:, 4] - w[4]) <= 1e-3) & ~used
-        k = np.flatnonzero(ok)
-        if len(k):
-            used[k[0]] = True
-            matched += 1
-    print(f"\nfp16 predict: {len(got)} boxes, oracle {len(res)}, matched {matched}")
-    assert matched >= 0.97 * max(len(got), len(res)), (matched, len(got), len(res))
+    # fp16: the difference to the oracle is decomposed, as the C2 tests do.
+    # 1. the same chain predict() ran, step by step on the device: letterbox -> fp16 forward ->
+    #    decode_box -> non_max_suppression; predict's boxes are exactly this chain's rows
+    from ycx.detect import decode_box, nms_device, non_max_suppression
+    from helpers import decoded_flip_report  # noqa: E402
+    m = Model(net_cfg, ANCHORS, 1, precision='fp16').eval()
+    m.load_state_dict(sd)
+    m.to('cuda:0')
+    xd = letterbox_gpu(img, (size, size), device='cuda:0').unsqueeze(0)
+    assert torch.equal(xd.cpu(), x)  # the device letterbox is bit-exact to the restatement
+    heads_dev = m(xd)
+    dec_dev = torch.cat(decode_box(heads_dev, A, MASK, 1, (size, size)), 1)
+    mine = non_max_suppression(dec_dev.clone(), 1, (size, size), np.array(img.shape[0:2]), True, 0.3, 0.3)[0]
+    assert len(mine) == len(got)
+    for tb, row in zip(got, mine):
+        y1, x1, y2, x2 = row[0], row[1], row[2], row[3]
+        assert [tb.left, tb.top, tb.right, tb.bottom] == [
+            max(0, int(np.floor(x1))), max(0, int(np.floor(y1))),
+            min(img.shape[1], int(np.floor(x2))), min(img.shape[0], int(np.floor(y2)))]
+        assert float(tb.score) == float(row[4] * row[5])
+    # 2. NMS: the oracle's greedy chain on the DEVICE's own decoded tensor keeps exactly the
+    #    device's rows, in the device's order (bit-exact keep indices on identical inputs)
+    _, keep_d, kc_d = nms_device(dec_dev.clone(), 1, 0.3, 0.3)
+    keep_d = keep_d[0, :int(kc_d[0])].cpu().numpy().astype(np.int64)
+    own = ref_post.nms_keep_rows(dec_dev.cpu().clone(), 1, 0.3, 0.3)[0][0].numpy()
+    assert np.array_equal(keep_d, own), (len(keep_d), len(own))
+    # 3. forward: the decoded box / objectness / class-confidence tensors within north_star's 1e-3
+    #    (dec itself is xyxy now: non_max_suppression rewrote it in place, detect.py:98-103)
+    dec = torch.cat(ref_post.decode_box(heads, A, MASK, 1, (size, size)), 1)
+    errs = {k: rel_err(dec_dev[0, :, sl].cpu(), dec[0, :, sl]) for k, sl in
+            (('box', slice(0, 4)), ('obj', slice(4, 5)), ('cls', slice(5, 6)))}
+    assert max(errs.values()) < 1e-3, errs
+    # 4. end to end: every keep-set difference between the two chains is caused by the
+    #    forward's perturbation (a threshold crossing, a score swap or an IoU crossing)
+    rep = decoded_flip_report(dec_dev[0], dec[0], 1, 0.3, 0.3)
+    print(f"\nfp16 predict at {size} ({hw}): {len(got)} boxes, oracle {len(res)}; decoded err {errs}; {rep}")
+    assert rep['member_far'] == 0 and rep['cls_flips'] == 0, rep
+    assert rep['unexplained_flips'] == 0, rep
 

@@ -2,13 +2,15 @@
 
 Tolerances (max |gpu - ref| / max |ref| per output tensor):
   f32 parity mode : 1e-3  (north_star: 1e-3 relative on box/confidence tensors)
-  fp16            : 2e-3 on raw tensors (IEEE half activations/weights on the f16 MFMA; a G1
+  fp16            : 1e-3 on raw tensors (IEEE half activations/weights on the f16 MFMA; a G1
                            net that ends in an activation carries that value's own fp16
-                           rounding, 2^-11 relative, measured r03 <= 0.0009; the heads of
-                           yolov7-tiny at 640 measured 0.0013); the DECODED box / objectness /
-                           class-confidence tensors north_star names are held to 1e-3
-                           (test_g2_decoded_fp16, test_yolov7_640_vs_oracle, C2 in
-                           test_gpu_configs.py)
+                           rounding, 2^-11 relative, measured r03 <= 0.0009; yolov7_160 heads
+                           4.4e-4). One documented exception: the RAW logits of yolov7-tiny
+                           at 640 (LeakyReLU, 1.21-1.34e-3 measured r03) are held to 1.5e-3;
+                           the DECODED box / objectness / class-confidence tensors north_star
+                           names are held to 1e-3 everywhere, that net included (6.4e-4 /
+                           4.2e-4 / 4.6e-4: test_g2_decoded_fp16, test_yolov7_640_vs_oracle,
+                           C2 in test_gpu_configs.py)
   bf16            : 2.5e-2 (bf16 activations/weights drift ~0.5 % median, up to 1.25 % of
                            max-abs end to end through 100+ layers: measured r02 max 0.0125)
 """
@@ -24,7 +26,8 @@ from ycx.utils.synth import synthetic_images
 pytestmark = pytest.mark.gpu
 
 F32_TOL, BF16_TOL = 1e-3, 2.5e-2   # bf16 measured r02: <= 0.0125 (G2 tiny_640), yolov7 heads ~0.005
-F16_TOL = 2e-3
+F16_TOL = 1e-3
+F16_RAW_TOL = {'tiny_640': 1.5e-3}  # raw LeakyReLU-net logits only; decoded: 1e-3 (module doc)
 G1_NAMES = ['conv_k3s1_cin32', 'conv_k3s2_cin32', 'conv_k1_cin64', 'conv_leaky', 'stem_s2_leaky', 'pools',
             'upsample_concat', 'upsample_shared', 'sppcspc', 'repconv', 'csp_blocks', 'detect', 'idetect',
             'upsample_offset', 'iauxdetect']
@@ -68,6 +71,8 @@ def test_g1_ops(device, manifest, g1, name, precision, tol):
 @pytest.mark.parametrize('name', ['yolov7_160', 'tiny_640'])
 def test_g2_nets(device, manifest, g2, name, precision, tol):
     e = manifest['g2'][name]
+    if precision == 'fp16':
+        tol = F16_RAW_TOL.get(name, tol)
     m, _ = make_model(e['net'], e['nc'], e['w_seed'], precision)
     m.to(device)
     x = synthetic_images(*e['shape'], seed=e['img_seed']).to(device)
@@ -294,3 +299,53 @@ def test_concurrent_detector_dropped_in_flight(device):
     del junk
     for d, k, c in outs:
         assert torch.equal(c, c_ref) and torch.equal(k, k_ref) and torch.equal(d, d_ref)
+
+
+@pytest.mark.parametrize('net,nc', [('yolov7', 80), ('yolov7-tiny', 1)])
+def test_fp16_range_guard(device, net, nc):
+    """VERDICT r3 weak 1 / ADVICE r3: the fp16 plan (the Model default) must never return
+    inf / NaN silently. A synthetic checkpoint whose third conv's BN scale is multiplied by
+    1e5 drives that layer's activations past 65504 (fine in fp32 / bf16, inf in fp16):
+      - the fused Detector fast path sets its device flag and check() raises YcxRangeError
+        (ConcurrentDetector.check() likewise, over all slots);
+      - Model.forward warns and re-plans itself in bf16, and the heads it then returns are
+        finite and equal to a bf16 Model's.
+    The unmodified checkpoint raises nothing (the flag stays 0)."""
+    from ycx import _lib as L
+    from ycx.detect import ConcurrentDetector, Detector
+    mask = [[6, 7, 8], [3, 4, 5], [0, 1, 2]]
+    m, sd = make_model(net, nc, 0, 'fp16')
+    m.to(device)
+    shape = (2, 3, 160, 160)
+    x = synthetic_images(*shape, seed=9).to(device)
+    det = Detector(m, shape, device, ANCHORS, mask, conf_thres=0.3, nms_thres=0.45, max_det=300)
+    assert det.fused
+    det(x)
+    det.check()  # in range: no error
+    assert not det.overflowed()
+    det.close()
+    bn = [k for k in sd if k.endswith('.bn.weight')][2]
+    big = dict(sd)
+    big[bn] = sd[bn] * 1e5
+    m.load_state_dict(big)
+    m.to(device)
+    det = Detector(m, shape, device, ANCHORS, mask, conf_thres=0.3, nms_thres=0.45, max_det=300)
+    det(x)
+    assert det.overflowed()
+    with pytest.raises(L.YcxRangeError, match='non-finite'):
+        det.check()
+    det.close()
+    cd = ConcurrentDetector(m, shape, device, ANCHORS, mask, depth=2, conf_thres=0.3, nms_thres=0.45)
+    cd.submit(x)
+    with pytest.raises(L.YcxRangeError):
+        cd.check()
+    cd.close()
+    with pytest.warns(RuntimeWarning, match='overflowed'):
+        outs = m(x)
+    assert m.precision == 'bf16'
+    assert all(bool(torch.isfinite(o).all()) for o in outs)
+    mb, _ = make_model(net, nc, 0, 'bf16')
+    mb.load_state_dict(big)
+    mb.to(device)
+    for a, b in zip(outs, mb(x)):
+        assert torch.equal(a, b)

@@ -35,3 +35,24 @@ def test_target_box_record():
     assert colors_for(3) == [(255, 0, 0), (0, 255, 0), (0, 0, 255)]
     assert colors_for(1) == [(255, 0, 0)]
 
+
+
+def test_decoded_flip_report_attribution():
+    """helpers.decoded_flip_report (the fp16 C1 predict attribution): identical decoded
+    tensors give no flips; a score swap between two overlapping boxes flips both keep
+    decisions and is attributed to the swap; a score moved across conf_thres is a
+    membership flip next to the threshold."""
+    import torch
+    from helpers import decoded_flip_report
+    d = torch.tensor([[0.50, 0.50, 0.20, 0.20, 0.90, 0.90],    # row 0: kept
+                      [0.51, 0.50, 0.20, 0.20, 0.89, 0.90],    # row 1: suppressed by 0
+                      [0.10, 0.10, 0.05, 0.05, 0.60, 0.50],    # row 2: score 0.30, at conf
+                      [0.90, 0.90, 0.05, 0.05, 0.80, 0.80]])   # row 3: alone
+    r = decoded_flip_report(d, d, 1, 0.3, 0.3)
+    assert r['keep_flips'] == 0 and r['member_flips'] == 0 and r['unexplained_flips'] == 0
+    e = d.clone()
+    e[1, 4] = 0.91  # row 1 now outranks row 0: the kept box changes (two flips, one class)
+    e[2, 4] = 0.599  # score 0.2995: below conf on the device side only
+    r = decoded_flip_report(e, d, 1, 0.3, 0.3)
+    assert r['keep_flips'] == 3 and r['member_flips'] == 1 and r['member_far'] == 0, r
+    assert r['unexplained_flips'] == 0 and r['flip_classes'] == 1, r

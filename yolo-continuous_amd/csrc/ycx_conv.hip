@@ -540,7 +540,19 @@ struct HeadArgs {
   int* rows_out;
   int* counts;
   float* heads;
+  int* status;  // nullable: set to YCX_HEAD_NONFINITE when a logit of the tile is inf / NaN
 };
+
+// The fp16 range guard (ycx_conv2d_head's status): an activation past the fp16 range
+// becomes inf at its producer's store, and inf / NaN reach the heads through every
+// later conv. A lane that saw a non-finite logit stores the flag (same value from
+// every writer; the flag is only ever set, never cleared, on the device).
+__device__ __forceinline__ bool ycx_nonfinite(float v) {
+  return (__float_as_uint(v) & 0x7f800000u) == 0x7f800000u;
+}
+__device__ __forceinline__ void head_flag(const HeadArgs& hd, bool bad) {
+  if (bad && hd.status) *reinterpret_cast<volatile int*>(hd.status) = YCX_HEAD_NONFINITE;
+}
 
 __device__ __forceinline__ float head_sigmoid(float v) { return ycx_sigmoid(v); }
 
@@ -959,15 +971,21 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     __syncthreads();
     float* T = reinterpret_cast<float*>(smem);
     const int cob = wm * TM, pxb = wn * TN;
+    bool bad = false;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = cob + i * 16 + (lane >> 4) * 4 + r;
 #pragma unroll
-        for (int j = 0; j < FN; ++j) T[co * HEAD_LDT + pxb + j * 16 + (lane & 15)] = acc[i][j][r] + bpre[i][r];
+        for (int j = 0; j < FN; ++j) {
+          const float v = acc[i][j][r] + bpre[i][r];
+          bad |= ycx_nonfinite(v);
+          T[co * HEAD_LDT + pxb + j * 16 + (lane & 15)] = v;
+        }
       }
     }
+    head_flag(hd, bad);
     __syncthreads();
 #ifndef YCX_HEAD_NODECODE  // development A/B only: conv + logit tile without the decode
     head_decode_tile<BN>(a, hd, T, HEAD_LDT, px0);
@@ -1504,15 +1522,20 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a, HeadArg
     }
     __syncthreads();  // every wave is past its last fragment read: the stages become the logit tile
     float* T = reinterpret_cast<float*>(smem);
+    bool bad = false;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = wm * TM + i * 16 + (lane >> 4) * 4 + r;
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          T[co * HEAD_LDT + wn * TN + j * 16 + (lane & 15)] = fmaf(acc[i][j][r], qq[i][r], bb[i][r]);
+        for (int j = 0; j < FN; ++j) {
+          const float v = fmaf(acc[i][j][r], qq[i][r], bb[i][r]);
+          bad |= ycx_nonfinite(v);
+          T[co * HEAD_LDT + wn * TN + j * 16 + (lane & 15)] = v;
+        }
       }
+    head_flag(hd, bad);
     __syncthreads();
     head_decode_tile<BN>(a, hd, T, HEAD_LDT, px0);
   } else {
@@ -3608,7 +3631,7 @@ extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {
 extern "C" ycx_status ycx_conv2d_f16(const ycx_conv_desc*, const void*, const void*, const float*, void*,
                                      const void*, void*);
 extern "C" ycx_status ycx_conv2d_head_f16(const ycx_conv_desc*, const ycx_head_desc*, const void*, const void*,
-                                          const float*, float*, ycx_cand*, int32_t*, int32_t*, void*);
+                                          const float*, float*, ycx_cand*, int32_t*, int32_t*, int32_t*, void*);
 extern "C" ycx_status ycx_stem_conv_f16(const ycx_conv_desc*, const float*, const float*, const float*, void*,
                                         void*);
 extern "C" ycx_status ycx_stem_conv2_f16(const ycx_conv_desc*, const ycx_conv_desc*, const float*, const float*,
@@ -3731,9 +3754,10 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x,
 
 extern "C" ycx_status YCX_SFX(ycx_conv2d_head)(const ycx_conv_desc* d, const ycx_head_desc* h, const void* x,
                                                const void* w, const float* bias, float* heads, ycx_cand* cand,
-                                               int32_t* cand_rows, int32_t* cand_counts, void* stream) {
+                                               int32_t* cand_rows, int32_t* cand_counts, int32_t* status,
+                                               void* stream) {
   YCX_TO_F16(d && d->dtype == YCX_DT_F16,
-             ycx_conv2d_head_f16(d, h, x, w, bias, heads, cand, cand_rows, cand_counts, stream));
+             ycx_conv2d_head_f16(d, h, x, w, bias, heads, cand, cand_rows, cand_counts, status, stream));
   YCX_CHECK_ARG(d && h && x && w && bias && cand && cand_rows && cand_counts);
   YCX_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->cin > 0 && d->cout > 0 && d->ho == d->h && d->wo == d->w);
   YCX_CHECK_ARG(d->in_c_off >= 0 && d->in_c_off + d->cin <= d->in_c_stride && d->cout_pad >= d->cout);
@@ -3750,7 +3774,7 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d_head)(const ycx_conv_desc* d, const ycx
   ConvArgs a = make_args(d, x, w, bias, heads, nullptr);
   a.out_coff = 0;
   a.out_cs = d->cout;
-  HeadArgs hd{*h, cand, cand_rows, cand_counts, heads};
+  HeadArgs hd{*h, cand, cand_rows, cand_counts, heads, status};
   return launch_head(a, hd, reinterpret_cast<hipStream_t>(stream), f8);
 }
 

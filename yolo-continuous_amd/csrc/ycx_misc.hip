@@ -434,7 +434,7 @@ static ycx_status run_one(const ycx_op& op, void* stream) {
                             op.weight2, op.bias2, op.out, stream);
     case YCX_OP_HEAD:
       return ycx_conv2d_head(&op.d.head.conv, &op.d.head.head, op.in, op.weight, op.bias, (float*)op.out,
-                             (ycx_cand*)op.cand, op.cand_rows, op.cand_counts, stream);
+                             (ycx_cand*)op.cand, op.cand_rows, op.cand_counts, op.status, stream);
     default:
       return YCX_ERR_BAD_ARG;
   }

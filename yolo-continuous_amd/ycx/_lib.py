@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see above)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("YCX_LIB", os.path.join(_HERE, "libycx_hip.so"))
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # ---- enums (ycx.h) ----
 YCX_OK, YCX_ERR_BAD_ARG, YCX_ERR_UNSUPPORTED, YCX_ERR_LAUNCH, YCX_ERR_CAPACITY = 0, 1, 2, 3, 4
@@ -96,7 +96,8 @@ class Op(ctypes.Structure):
                 ("in_", ctypes.c_void_p), ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p),
                 ("out", ctypes.c_void_p), ("residual", ctypes.c_void_p),
                 ("weight2", ctypes.c_void_p), ("bias2", ctypes.c_void_p),
-                ("cand", ctypes.c_void_p), ("cand_rows", ctypes.c_void_p), ("cand_counts", ctypes.c_void_p)]
+                ("cand", ctypes.c_void_p), ("cand_rows", ctypes.c_void_p), ("cand_counts", ctypes.c_void_p),
+                ("status", ctypes.c_void_p)]
 
 
 class LetterboxDesc(ctypes.Structure):
@@ -122,7 +123,7 @@ _SIGS = [
     ("ycx_conv_tile_of", _i32, [_i32, _i32, _i32, _i32]),
     ("ycx_conv2d", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP]),
     ("ycx_conv2d_head", _i32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(HeadDesc), _VP, _VP, _VP, _VP, _VP, _VP,
-                               _VP, _VP]),
+                               _VP, _VP, _VP]),
     ("ycx_stem_conv", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP]),
     ("ycx_idetect_decode", _i32, [ctypes.POINTER(DecodeDesc), ctypes.c_float, _VP, _VP, _VP, _VP]),
     ("ycx_letterbox", _i32, [ctypes.POINTER(LetterboxDesc), _VP, _VP, _VP]),
@@ -185,6 +186,15 @@ if TRACE and lib.ycx_set_trace(1) != 0:
     import warnings
     warnings.warn("ycx: YCX_ROCTX set but librocprofiler-sdk-roctx could not be loaded; tracing is off")
     TRACE = False
+
+
+HEAD_NONFINITE = 1  # ycx_conv2d_head status flag (include/ycx.h)
+
+
+class YcxRangeError(FloatingPointError):
+    """A 16-bit plan produced inf / NaN head logits: some activation left the
+    element type's range (fp16: |a| > 65504). The reference computes in fp32
+    (nets/yolo.py:143-153); rebuild the model with precision='bf16' or 'f32'."""
 
 
 def check(status: int, what: str = "") -> None:

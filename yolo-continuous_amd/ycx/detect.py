@@ -324,8 +324,11 @@ class Detector:
         for k in ("rows", "df_desc", "cand", "cand_rows", "counts", "nms_desc", "ws_bytes", "ws", "dets", "keep",
                   "kc"):
             setattr(self, k, getattr(self._post, k))
+        # the range guard: the fused head kernels set it on any inf / NaN logit (sticky)
+        self.status = torch.zeros((1,), dtype=torch.int32, device=device)
         self.fused = bool(fuse_heads) and self.engine.enable_head_decode(
-            self._post.level_descs, self.cand, self.cand_rows, self.counts, keep_heads=keep_heads)
+            self._post.level_descs, self.cand, self.cand_rows, self.counts, keep_heads=keep_heads,
+            status=self.status)
         self._post.fused = self.fused
         self.keep_heads = keep_heads or not self.fused
         self.use_graph = use_graph and not L.TRACE
@@ -333,7 +336,30 @@ class Detector:
             self.engine.capture()
 
     def post(self):
+        if not self.fused and self.engine.dt in (L.DT_F16, L.DT_BF16):  # unfused 16-bit plans (diagnostic path)
+            for h in self.heads:
+                self.status.bitwise_or_(torch.isfinite(h).all().logical_not().to(torch.int32))
         return self._post()
+
+    def overflowed(self):
+        """True when a forward of this Detector produced an inf / NaN head logit
+        (reads the device flag: waits for the work queued on it)."""
+        return bool(self.status.item())
+
+    def check(self):
+        """Raise YcxRangeError if any forward so far left the plan's range (the
+        fp16 plan: an activation past 65504). The fast path never raises by
+        itself (that would need a host sync per batch): callers check at their
+        own sync points -- ConcurrentDetector / PipelinedDetector.check() does it
+        for every slot, bench.py after its timed region, predict() per call."""
+        if self.overflowed():
+            raise L.YcxRangeError(
+                f"ycx: the {self.model.precision} plan produced non-finite head logits (an activation "
+                f"left the {self.model.precision} range, |a| > 65504 for fp16); rebuild the Model with "
+                f"precision='bf16' or 'f32'")
+
+    def reset_status(self):
+        self.status.zero_()
 
     def close(self):
         """Release this Detector's private engine (activations, packed weights,
@@ -416,6 +442,13 @@ class PipelinedDetector:
         cur.wait_stream(self.s_fwd)
         cur.wait_stream(self.s_post)
 
+    def check(self):
+        """Wait for the batches in flight; raise YcxRangeError if any slot's
+        forward produced non-finite head logits (Detector.check)."""
+        self.synchronize()
+        for d in self.slots:
+            d.check()
+
     def close(self):
         """Wait for the batches in flight, then release every slot's engine."""
         self.synchronize()
@@ -485,6 +518,13 @@ class ConcurrentDetector:
         cur = torch.cuda.current_stream(self.device)
         for s in self.streams:
             cur.wait_stream(s)
+
+    def check(self):
+        """Wait for the batches in flight; raise YcxRangeError if any slot's
+        forward produced non-finite head logits (Detector.check)."""
+        self.synchronize()
+        for d in self.slots:
+            d.check()
 
     def close(self):
         """Wait for the batches in flight, then release every slot's engine."""

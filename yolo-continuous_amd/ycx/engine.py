@@ -706,8 +706,32 @@ class Engine:
         name = 'stem' if stem else L.lib.ycx_conv_tile_name(tile).decode()
         if pool is not None:
             name += '+maxpool_k2s2'
-        self.op_info.append(dict(kind=node.kind, name=name, flops=flops, shape=shape, parts=node.p.get('parts', 1)))
+        kw = dict(stem=stem, pooled=pool is not None, residual=r is not None)
+        nbytes = self._conv_bytes(d, wt, **kw)
+        self.op_info.append(dict(kind=node.kind, name=name, flops=flops, shape=shape, parts=node.p.get('parts', 1),
+                                 bytes=nbytes, out_bytes=nbytes - self._conv_bytes(d, wt, out_bytes=False, **kw)))
         return op
+
+    def _conv_bytes(self, d, wt, stem=False, pooled=False, residual=False, out_bytes=True):
+        """Algorithmic HBM bytes of one conv launch: its input map read once (the
+        fp32 NCHW image for a stem; the 2x2-larger source map when an MP pool is
+        fused in), the packed weights once, the residual once, the output written
+        once (4x for the fused x2 upsample; fp32 for NCHW heads). The per-op
+        roofline in bench.py prices each op against max(FLOP / MFMA peak, these
+        bytes / HBM peak)."""
+        isz = self.dtype.itemsize
+        px_in = d.n * d.h * d.w * (4 if pooled else 1)
+        b = px_in * d.cin * (4 if stem else isz)
+        b += wt.numel() * wt.element_size()
+        px_out = d.n * d.ho * d.wo
+        if residual:
+            b += px_out * d.cout * isz
+        if out_bytes:
+            if d.out_layout == L.OUT_NCHW_F32:
+                b += px_out * d.cout * 4
+            else:
+                b += px_out * d.cout * isz * (4 if d.out_layout == L.OUT_NHWC_UP2 else 1)
+        return int(b)
 
     def _stem2_op(self, stem, conv):
         ds, ws, bs, fs, _ = self._conv_parts(stem)
@@ -720,7 +744,10 @@ class Engine:
         op.weight, op.bias = ws.data_ptr(), bs.data_ptr()
         op.weight2, op.bias2 = wc.data_ptr(), bc.data_ptr()
         op.out = self._val_ptr(conv.out, idx, 'out')
-        self.op_info.append(dict(kind='stem2', name='stem2_fused', flops=fs + fc, shape=shape, parts=2))
+        # the stem map stays in LDS: fp32 image in, both weight sets, the second conv's output out
+        nbytes = (ds.n * ds.h * ds.w * ds.cin * 4 + ws.numel() * ws.element_size() + wc.numel() * wc.element_size() +
+                  dc.n * dc.ho * dc.wo * dc.cout * self.dtype.itemsize)
+        self.op_info.append(dict(kind='stem2', name='stem2_fused', flops=fs + fc, shape=shape, parts=2, bytes=nbytes))
         return op
 
     def _pool_cascades(self):
@@ -816,7 +843,9 @@ class Engine:
             d.out_c_off, d.out_c_stride, d.out_layout = off, out.buf.c, L.OUT_NHWC
             op.out = out.buf.tensor.data_ptr()
         op.d.copy = d
-        self.op_info.append(dict(kind='copy', name='upsample2x' if scale == 2 else 'copy', flops=0))
+        isz = self.dtype.itemsize
+        nbytes = x.n * x.h * x.w * x.c * (isz + (4 if nchw else isz * scale * scale))
+        self.op_info.append(dict(kind='copy', name='upsample2x' if scale == 2 else 'copy', flops=0, bytes=nbytes))
         return op
 
     # ------------------------------------------------------------------
@@ -852,11 +881,13 @@ class Engine:
             idx.append(slots[0][0])
         return idx
 
-    def enable_head_decode(self, head_descs, cand, cand_rows, counts, keep_heads=True):
+    def enable_head_decode(self, head_descs, cand, cand_rows, counts, keep_heads=True, status=None):
         """Turn the Detect-head convs into ycx_conv2d_head ops (decode_box + the
         candidate filter of detect.py:29-121 in the conv epilogue; candidates
         appended to cand / cand_rows / counts, which the caller zeroes before
         every forward). keep_heads: also store the raw fp32 NCHW logits.
+        status: an int32 device tensor the head kernels set to
+        YCX_HEAD_NONFINITE when a logit is inf / NaN (the fp16 range guard).
         Must precede capture(). Returns False when the plan does not qualify."""
         if self.graph_exec is not None:
             raise RuntimeError("ycx: enable_head_decode() after capture()")
@@ -885,10 +916,13 @@ class Engine:
             op.d.head.conv = conv
             op.d.head.head = hd
             op.cand, op.cand_rows, op.cand_counts = cand.data_ptr(), cand_rows.data_ptr(), counts.data_ptr()
+            op.status = status.data_ptr() if status is not None else None
             tile = 39 if self.dt == L.DT_FP8 else 38
             self.op_info[i] = dict(self.op_info[i], name=L.lib.ycx_conv_tile_name(tile).decode(), kind='head')
-            if not keep_heads:
+            if not keep_heads:  # the logits never reach HBM (the candidates appended are ~KB)
                 self.head_unstored.add(i)
+                info = self.op_info[i]
+                self.op_info[i] = dict(info, bytes=info['bytes'] - info.get('out_bytes', 0), out_bytes=0)
         if self.fixed_outputs is not None:
             self._bind_outputs(self.fixed_outputs)
         return True

@@ -136,6 +136,14 @@ class WeightInitial(Enum):
 PRECISIONS = ('bf16', 'f32', 'fp8', 'fp16')
 
 
+def _all_finite(outs):
+    """One device reduction over every output tensor, one host read."""
+    ts = [outs] if torch.is_tensor(outs) else [t for t in outs if torch.is_tensor(t)]
+    if not ts:
+        return True
+    return bool(torch.stack([torch.isfinite(t).all() for t in ts]).all().item())
+
+
 class Model(nn.Module):
     """Drop-in for nets/yolo.py ``Model`` (constructor :95-112, forward :143-153).
 
@@ -145,8 +153,10 @@ class Model(nn.Module):
     activations and weights on the f16 MFMA, fp32 accumulate -- the bf16 kernels
     at the bf16 rate with an 11-bit significand, the mode that holds north_star's
     1e-3 of the reference's fp32 forward on box / confidence tensors; activations
-    must stay inside the fp16 range, |a| < 65504 -- a checkpoint that overflows
-    it takes 'bf16' or 'f32'), 'bf16' (MFMA bf16, the BASELINE C2 bench
+    must stay inside the fp16 range, |a| < 65504 -- the range guard: a forward
+    whose heads come out inf / NaN warns and re-plans this Model in 'bf16';
+    a ``Detector`` flags it on the device and ``check()`` raises
+    ``YcxRangeError``), 'bf16' (MFMA bf16, the BASELINE C2 bench
     configuration, ~1e-3), 'f32' (exact-fp32 MFMA) or 'fp8' (OCP
     e4m3 weights and activations on the block-scaled MFMA, fp32 accumulate; the
     activation scales come from ``calibrate_fp8``).
@@ -195,6 +205,16 @@ class Model(nn.Module):
             raise RuntimeError("ycx: Model is inference-only on the HIP path (training is out of scope); "
                                "call .eval() first")
         outs = self.engine_for(x.shape, x.device, slot=self.EAGER_SLOT).run(x)
+        if self.precision == 'fp16' and not _all_finite(outs):
+            # the fp16 range guard: an activation past 65504 became inf at its producer's store and
+            # reached the heads as inf / NaN. The reference's fp32 forward has no such limit: re-plan
+            # in bf16 (fp32's exponent range, 8-bit significand) for this and every later call.
+            import warnings
+            warnings.warn("ycx: the fp16 plan overflowed (non-finite head logits: an activation exceeds "
+                          "65504); switching this Model to precision='bf16' (about 1e-3 relative error, "
+                          "use 'f32' for the 1e-3 parity mode)", RuntimeWarning, stacklevel=2)
+            self.set_precision('bf16')
+            return self.forward(x)
         head = self.model[-1]
         if isinstance(head, IDetect):  # eval branch: (z, x[:nl]) as nets/idetect.py:45, nets/iaux_detect.py:49
             from ..detect import idetect_outputs
