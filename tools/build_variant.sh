@@ -12,6 +12,6 @@ mkdir -p build/var
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -Wno-unused-function -DYCX_ELT_F16 "$@" \
   -c ycx_conv.hip -o build/var/ycx_conv_f16_$NAME.o 2>/dev/null
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC build/var/ycx_conv_$NAME.o build/var/ycx_conv_f16_$NAME.o \
-  build/ycx_misc.o build/ycx_post.o build/ycx_nms.o build/ycx_image.o -L/opt/rocm/lib -lrocprofiler-sdk-roctx \
-  -Wl,-rpath,/opt/rocm/lib -o ../ycx/libycx_$NAME.so
+  build/ycx_misc.o build/ycx_post.o build/ycx_nms.o build/ycx_image.o -ldl \
+  -o ../ycx/libycx_$NAME.so
 echo yolo-continuous_amd/ycx/libycx_$NAME.so

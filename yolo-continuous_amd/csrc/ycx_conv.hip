@@ -659,11 +659,7 @@ __device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const fl
       if (tid < 2) {
         int tot = 0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += s_cnt[2 * w + tid];
-#ifndef YCX_HEAD_NOATOMIC  // development A/B only (slots = rows: wrong counts)
         s_cnt[32 + tid] = tot ? atomicAdd(hd.counts + n0 + tid, tot) : 0;
-#else
-        s_cnt[32 + tid] = 0;
-#endif
       }
       __syncthreads();
       if (pass) {
@@ -987,9 +983,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     }
     head_flag(hd, bad);
     __syncthreads();
-#ifndef YCX_HEAD_NODECODE  // development A/B only: conv + logit tile without the decode
     head_decode_tile<BN>(a, hd, T, HEAD_LDT, px0);
-#endif
     done = true;
   }
   if constexpr (FM % 2 == 0 && !HEAD) {
@@ -1000,182 +994,6 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     }
   }
   if (!HEAD && !done) epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
-#ifdef YCX_GLDS_STAMP
-  {
-    const unsigned long long e = stamp_issue();
-    stamp_sync();
-    st_sum[6] = e - st_prev;
-    st_sum[7] = e - st_start;
-  }
-  if (lane < 8) {
-    unsigned long long v = 0;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) v = lane == b ? st_sum[b] : v;
-    atomicAdd(&g_glds_stamp[(wid & 15) * 8 + lane], v);
-  }
-  if (tid == 0) atomicAdd(&g_glds_stamp[128], 1ull);
-#endif
-}
-
-// -------------------------------------------------------------------------
-// Tile 40: 256 (cout) x 256 (px) per workgroup, 1024 threads (16 waves as 4 x 4, each
-// 64 x 64 = 4 x 4 fragments), 32-deep K stages, NS = 4 stages in LDS (128 KiB, one
-// workgroup per CU) with three in flight. Why: the 128 x 128 two-per-CU tile (16) is
-// bound by the CU's LDS-DMA intake (32 KiB per 2.1 MFLOP: at the ~55-68 GB/s a CU takes
-// in, MFMA stays ~40 % busy); a 256 x 256 tile needs half the bytes per
-// FLOP (32 KiB per 4.2 MFLOP per stage) and three stages in flight hide the DMA latency
-// that a one-workgroup-per-CU two-stage ring exposed (tiles 24-26). Per stage and wave:
-// one 1 KiB LDS-DMA of A rows and one of B rows (16 rows x 64 B), 8 ds_read_b128, 16
-// MFMAs. Rows are 64 B with chunk swizzle swz<32> (conflict-free for the fragment reads:
-// every 16-lane group of ds_read_b128 covers the 64 banks once); the DMA applies it on
-// the source side. A rows are permuted as in conv_bf16_glds so the epilogue stores 16
-// bytes per lane and pixel (epilogue_regs8: bias, act, residual, x2 upsample).
-// -------------------------------------------------------------------------
-// Generalised (r03): conv_bigt<BM, BN, WM, WN, NS>, waves of 64 x 64 or 64 x 32 fragments, 32-deep
-// K stages, NS stages in LDS with NS - 1 in flight; each wave DMAs BM / (16 NW) A pieces and
-// BN / (16 NW) B pieces (16 rows x 64 B) per stage. Tile 40 = <256, 256, 4, 4, 4>; 41 =
-// <256, 128, 4, 2, 3> and 42 = <128, 256, 2, 4, 3> (72 KiB, two workgroups per CU, 25 % fewer
-// bytes per FLOP than tile 16 and two stages in flight per workgroup); 43 = <128, 128, 2, 4, 4>
-// (tile 16's bytes per FLOP, three stages in flight: the pipelining depth alone).
-template <int NSUB>
-__device__ __forceinline__ void vm_wait_stages(int younger) {  // younger stages of NSUB DMAs per wave may stay
-  if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NSUB) : "memory");
-  else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NSUB) : "memory");
-  else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSUB) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// DPOS: where a step issues the DMA of stage t + NS - 1: 0 right after the barrier, 1 after the
-// fragment reads, 2 between the MFMA halves, 3 after the MFMAs (NS >= 3 keeps a step of lead).
-template <int BM, int BN, int WM, int WN, int NS, int DPOS = 0>
-__global__ void __launch_bounds__(WM * WN * 64) conv_bigt(ConvArgs a) {
-  constexpr int NW = WM * WN, BK = 32, TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int A_PW = BM / (16 * NW), B_PW = BN / (16 * NW), LPS = A_PW + B_PW;
-  static_assert(TM == 64 && (TN == 64 || TN == 32) && A_PW >= 1 && B_PW >= 1 && NS >= 2 && NS <= 4, "tile shape");
-  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
-  const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
-  const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-#ifdef YCX_GLDS_STAMP
-  unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const unsigned long long st_start = stamp_issue();
-#endif
-  const int wm = wid / WN, wn = wid % WN;
-  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
-  int ct, pt;
-  ycx_tile_of(L, a.n_ct, a.nwg / a.n_ct, a.gc, ct, pt);
-  const int co0 = ct * BM, px0 = pt * BN;
-  const int pch = lane & 3;
-  const int w_bytes = a.Cout_pad * a.Ktot * 2, x_bytes = a.N * a.H * a.W * a.in_cs * 2;
-  int a_off[A_PW];
-#pragma unroll
-  for (int i = 0; i < A_PW; ++i) {
-    const int row = 16 * (wid + NW * i) + (lane >> 2);
-    const int f = (row % TM) >> 4, m = row & 15;
-    const int ch = (row / TM) * TM + 32 * (f >> 1) + 8 * (m >> 2) + 4 * (f & 1) + (m & 3);
-    a_off[i] = ((co0 + ch) * a.Ktot + ((pch ^ swz<BK>(row)) << 3)) * 2;
-  }
-  int b_iy0[B_PW], b_ix0[B_PW], b_base[B_PW];
-#pragma unroll
-  for (int i = 0; i < B_PW; ++i) {
-    const int row = 16 * (wid + NW * i) + (lane >> 2);
-    const int p = px0 + row;
-    const bool ok = p < a.M;
-    const int pp = ok ? p : 0;
-    const int n = pp / a.HoWo, rem = pp - n * a.HoWo;
-    const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
-    b_iy0[i] = ok ? oy * a.S - a.P : -(1 << 20);  // tail rows fail the bounds test: zeros
-    b_ix0[i] = ox * a.S - a.P;
-    b_base[i] = (((n * a.H + b_iy0[i]) * a.W + b_ix0[i]) * a.in_cs + a.in_coff + ((pch ^ swz<BK>(row)) << 3)) * 2;
-  }
-  int i_ky = 0, i_kx = 0, i_cb = 0;  // K position of the next stage to issue
-  auto issue = [&](int s, int slot) {
-    char* base = smem + slot * STAGE;
-#pragma unroll
-    for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * (BK * 2), base + (wid + NW * i) * 1024);
-    const int tap = ((i_ky * a.W + i_kx) * a.in_cs + i_cb) * 2;
-#pragma unroll
-    for (int i = 0; i < B_PW; ++i) {
-      const bool ok = (unsigned)(b_iy0[i] + i_ky) < (unsigned)a.H && (unsigned)(b_ix0[i] + i_kx) < (unsigned)a.W;
-      buf_lds16(X, x_bytes, ok ? b_base[i] + tap : 0x7FFFFFF0, 0, base + A_BYTES + (wid + NW * i) * 1024);
-    }
-    i_cb += BK;
-    if (i_cb == a.Cin) {
-      i_cb = 0;
-      if (++i_kx == a.KW) { i_kx = 0; ++i_ky; }
-    }
-  };
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nt = a.nsteps;
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < nt) issue(s, s);
-#ifdef YCX_GLDS_STAMP
-  unsigned long long st_prev = stamp_issue();
-  stamp_sync();
-  st_sum[0] = st_prev - st_start;
-#endif
-  for (int t = 0; t < nt; ++t) {
-    // stage t is complete once at most its younger stages' DMAs remain
-    vm_wait_stages<LPS>(min(NS - 2, nt - 1 - t));
-    STAMP(1);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    STAMP(2);
-    if (DPOS == 0 && t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);  // the slot of stage t - 1, read by all
-    STAMP(3);
-    const char* A = smem + (t % NS) * STAGE;
-    const char* B = A + A_BYTES;
-    eltx8 af[FM], bfr[FN];
-    const int c = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int r = wm * TM + i * 16 + (lane & 15);
-      af[i] = *reinterpret_cast<const eltx8*>(A + r * 64 + ((c ^ swz<BK>(r)) << 4));
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int r = wn * TN + j * 16 + (lane & 15);
-      bfr[j] = *reinterpret_cast<const eltx8*>(B + r * 64 + ((c ^ swz<BK>(r)) << 4));
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (DPOS == 1 && t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);
-    __builtin_amdgcn_sched_barrier(0);
-    STAMP(4);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = YCX_MFMA16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      if (DPOS == 2 && i == FM / 2 - 1) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (DPOS == 3 && t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);
-    __builtin_amdgcn_sched_barrier(0);
-    STAMP(5);
-#ifdef YCX_GLDS_STAMP
-    stamp_sync();
-    st_sum[1] += st_t1 - st_prev;
-    st_sum[2] += st_t2 - st_t1;
-    st_sum[3] += st_t3 - st_t2;
-    st_sum[4] += st_t4 - st_t3;
-    st_sum[5] += st_t5 - st_t4;
-    st_prev = st_t5;
-#endif
-  }
-  f32x4 bpre[FM];
-  bias8_prefetch<FM>(a, co0 + wm * TM, lane, bpre);
-  epilogue_regs8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane, bpre);
 #ifdef YCX_GLDS_STAMP
   {
     const unsigned long long e = stamp_issue();
@@ -3248,14 +3066,14 @@ const TileInfo kTiles[] = {
     {64, 256, 64, "f8_halo3x3_ws_co64"},
     {256, 64, 64, "head_co256_px64_decode"},
     {256, 64, 128, "f8_head_co256_px64_decode"},
-    {256, 256, 32, "big_co256_px256_k32_s4"},
-    {256, 128, 32, "big_co256_px128_k32_s3"},
-    {128, 256, 32, "big_co128_px256_k32_s3"},
-    {128, 128, 32, "big_co128_px128_k32_s4"},
-    {256, 128, 32, "big_co256_px128_k32_s3_dma_after_reads"},
-    {256, 128, 32, "big_co256_px128_k32_s3_dma_mid_mfma"},
-    {256, 128, 32, "big_co256_px128_k32_s3_dma_after_mfma"},
-    {256, 256, 32, "big_co256_px256_k32_s4_dma_after_mfma"},
+    {256, 256, 32, "retired_big_co256_px256_k32_s4"},  // 40-47: retired (tools/experiments/conv_bigt_tiles40_47.patch)
+    {256, 128, 32, "retired_big_co256_px128_k32_s3"},
+    {128, 256, 32, "retired_big_co128_px256_k32_s3"},
+    {128, 128, 32, "retired_big_co128_px128_k32_s4"},
+    {256, 128, 32, "retired_big_co256_px128_k32_s3_dma_after_reads"},
+    {256, 128, 32, "retired_big_co256_px128_k32_s3_dma_mid_mfma"},
+    {256, 128, 32, "retired_big_co256_px128_k32_s3_dma_after_mfma"},
+    {256, 256, 32, "retired_big_co256_px256_k32_s4_dma_after_mfma"},
     {64, 320, 64, "halo3x3_band_co64_8x40_s2"},
     {128, 160, 64, "halo3x3_band_co128_4x40_s2"},
     {128, 128, 64, "halo3x3s2_wsr_co128"},
@@ -3355,18 +3173,6 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   if (a.pool) return YCX_ERR_UNSUPPORTED;
   hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST, NSB>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a,
                      HeadArgs{});
-  return ycx_launch_status();
-}
-
-// tiles 40-43: conv_bigt (32-deep K stages, NS - 1 in flight)
-template <int BM, int BN, int WM, int WN, int NS, int DPOS = 0>
-ycx_status launch_bigt(ConvArgs a, hipStream_t st) {
-  if (a.Cin % 32 || a.Cout_pad % BM || a.out_layout == YCX_OUT_NCHW_F32 || a.pool) return YCX_ERR_UNSUPPORTED;
-  a.nsteps = a.KH * a.KW * (a.Cin / 32);
-  a.n_ct = a.Cout_pad / BM;
-  a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
-  a.gc = glds_gc(a);
-  hipLaunchKernelGGL((conv_bigt<BM, BN, WM, WN, NS, DPOS>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a);
   return ycx_launch_status();
 }
 
@@ -3728,14 +3534,6 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x,
     case 24: return launch_glds<256, 256, 2, 4, false, 2>(a, st);
     case 25: return launch_glds<256, 128, 2, 4, false, 2>(a, st);
     case 26: return launch_glds<128, 256, 2, 4, false, 2>(a, st);
-    case 40: return launch_bigt<256, 256, 4, 4, 4>(a, st);
-    case 41: return launch_bigt<256, 128, 4, 2, 3>(a, st);
-    case 42: return launch_bigt<128, 256, 2, 4, 3>(a, st);
-    case 43: return launch_bigt<128, 128, 2, 4, 4>(a, st);
-    case 44: return launch_bigt<256, 128, 4, 2, 3, 1>(a, st);  // tile 41 with the DMA issue moved (DPOS)
-    case 45: return launch_bigt<256, 128, 4, 2, 3, 2>(a, st);
-    case 46: return launch_bigt<256, 128, 4, 2, 3, 3>(a, st);
-    case 47: return launch_bigt<256, 256, 4, 4, 4, 3>(a, st);  // tile 40 likewise
     case 48: return launch_halo<64, 2, 4, 2, 8, 40>(a, st);      // band halo tiles (40-wide maps)
     case 49: return launch_halo<128, 4, 2, 2, 4, 40>(a, st);
     case 50: return launch_s2wsr(a, st);

@@ -9,9 +9,9 @@
 //              bitonic-sorted across lanes and register slots, greedy scan with
 //              removed/kept bit masks, box i broadcast by readlane). Larger
 //              classes are queued as tasks (nms_fast / nms_wide, below; the r02
-//              general path nms_big under -DYCX_NMS_OLD_BIG).
-//  nms_big     one 1024-thread workgroup per large class (grid-strided task
-//              loop). (1) score sort (score desc, row asc = torchvision's stable
+//              general path nms_big is retired: tools/experiments/nms_big_r02.patch).
+//  (r02 design, kept by nms_fast / nms_wide) one 1024-thread workgroup per large
+//              class (grid-strided task loop). (1) score sort (score desc, row asc = torchvision's stable
 //              descending order) -> rank. (2) spatial counting sort: level =
 //              size octave of max(w, h) relative to the class extent, cell =
 //              centre cell in a 2^L x 2^L grid of that level. (3) per box, the
@@ -55,7 +55,7 @@ constexpr int kMaxRows = 131072;  // rows (candidates) per image
 #ifndef YCX_NMS_BIG_BLOCKS
 #define YCX_NMS_BIG_BLOCKS 256
 #endif
-constexpr int kBigBlocks = YCX_NMS_BIG_BLOCKS;   // nms_big grid (task-strided)
+constexpr int kBigBlocks = YCX_NMS_BIG_BLOCKS;   // nms_fast / nms_wide grid (task-strided)
 constexpr int kSlots = 16;        // highest-ranked suppressors cached per box
 #ifndef YCX_NMS_LEVELS
 #define YCX_NMS_LEVELS 7
@@ -63,7 +63,6 @@ constexpr int kSlots = 16;        // highest-ranked suppressors cached per box
 constexpr int kLevels = YCX_NMS_LEVELS;  // size octaves: level L holds max(w, h) < 2^-L of the class extent
 constexpr int kGridCells = ((1 << (2 * kLevels)) - 1) / 3;  // sum_{L < kLevels} 4^L
 constexpr int kWild = kGridCells; // one extra cell: boxes without a finite positive size
-constexpr int kCells = kGridCells + 1;
 
 #ifdef YCX_NMS_PROFILE
 // Development counters: shader cycles per nms_big phase, summed over tasks.
@@ -1848,170 +1847,6 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
 }
 
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_big(ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws,
-                                                    Thr thr, float t_lo, float inv_t, int all_pairs) {
-  constexpr int kLdsBytes = kBigLds;
-  constexpr int kLdsCellBytes = ((kCells * 4) + 255) & ~255;
-  // register sorts exchange through LDS when the keys fit (Pn <= kLdsBytes / 8), else the workspace
-  static_assert(kLdsBytes >= 8 * kBigThreads * 8 && kLdsBytes >= ((kCells * 4 + 255) & ~255) + 1024, "LDS budget");
-  static_assert(kLdsBytes >= 10 * kFastMax + 32 * kBigThreads, "fast path: sort buffers + rank table");
-  static_assert(kFSlots * 2 == kSlots * 4 && kFastMax <= 65536, "fast path: u16 slots in the general path's rows");
-  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
-  __shared__ int s_lv[kLevels][5];
-  __shared__ int s_ext[4];
-  __shared__ int s_w[kBigThreads / 64];
-  __shared__ int s_flag;
-  const int tid = threadIdx.x;
-  const int rows = d.rows_total;
-  const Layout L = layout(d.n, rows);
-  const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
-  const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks);
-  const int ntasks = hdr->nwide;
-  tasks += (size_t)d.n * L.max_tasks;  // the wide list
-  int* cells = reinterpret_cast<int*>(smem);
-  for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
-    const Task tk = tasks[t];
-    const Ptrs P = image_ptrs(ws, L, tk.img);
-    const ycx_cand* ci = cand + (size_t)tk.img * rows;
-    const int S = tk.S, off = tk.off;
-    int* bucket = P.bucket + off;
-#ifdef YCX_NMS_PROFILE
-    unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
-    if (tid == 0) atomicAdd(&g_nms_prof[7], 1ull);
-#endif
-    if (tid == 0) {
-      s_ext[0] = s_ext[1] = 0x7FFFFFFF;  // min x1, min y1
-      s_ext[2] = s_ext[3] = (int)0x80000000;  // max x2, max y2
-    }
-    if (tid < kLevels) {
-      s_lv[tid][0] = 0;
-      s_lv[tid][1] = s_lv[tid][2] = 0;  // +0.0f
-      s_lv[tid][3] = s_lv[tid][4] = 0x7F800000;  // +inf
-    }
-    const int Pn = max(next_pow2(S), kBigThreads);
-    // (1) rank = position in (score desc, row asc) order
-    unsigned long long* keys =
-        Pn <= kLdsBytes / 8 ? reinterpret_cast<unsigned long long*>(smem) : P.keys + 2 * (size_t)off;
-    switch (Pn / kBigThreads) {  // uniform
-      case 1: sort_class<1>(ci, bucket, S, keys); break;
-      case 2: sort_class<2>(ci, bucket, S, keys); break;
-      case 4: sort_class<4>(ci, bucket, S, keys); break;
-      case 8: sort_class<8>(ci, bucket, S, keys); break;
-      case 16: sort_class<16>(ci, bucket, S, keys); break;
-      default:  // > 16384 keys: workspace bitonic
-        for (int i = tid; i < Pn; i += kBigThreads) keys[i] = i < S ? make_key(ci[bucket[i]]) : ~0ull;
-        __syncthreads();
-        block_bitonic(keys, Pn);
-    }
-    YCX_PROF_MARK(0)
-    // (2) bucket in rank order; extent of the class's regular boxes
-    for (int r = tid; r < S; r += kBigThreads) {
-      const int row = (int)(unsigned)keys[r];
-      bucket[r] = row;
-      const ycx_cand b = ci[row];
-      if (b.x2 > b.x1 && b.y2 > b.y1 && b.x1 > -INFINITY && b.y1 > -INFINITY && b.x2 < INFINITY && b.y2 < INFINITY) {
-        atomicMin(&s_ext[0], f2o(b.x1));
-        atomicMin(&s_ext[1], f2o(b.y1));
-        atomicMax(&s_ext[2], f2o(b.x2));
-        atomicMax(&s_ext[3], f2o(b.y2));
-      }
-    }
-    __syncthreads();  // keys dead from here: LDS becomes the cell table
-    for (int k = tid; k < kCells; k += kBigThreads) cells[k] = 0;
-    __syncthreads();
-    const float X0 = o2f(s_ext[0]), Y0 = o2f(s_ext[1]);
-    const float E = fmaxf(o2f(s_ext[2]) - X0, o2f(s_ext[3]) - Y0);
-    const float inv = (E > 0.0f && E < INFINITY) ? 1.0f / E : 0.0f;  // 0: every box irregular
-    // (3) spatial counting sort: histogram (cell id parked in nsup[rank]), scan, scatter
-    for (int r = tid; r < S; r += kBigThreads) {
-      const ycx_cand b = ci[bucket[r]];
-      const Geo g = geometry(f32x4{b.x1, b.y1, b.x2, b.y2}, X0, Y0, inv, all_pairs);
-      P.nsup[off + r] = g.cell;
-      atomicAdd(&cells[g.cell], 1);
-    }
-    // per-level count / extreme sizes: reduced per wave, one LDS atomic per wave and level
-    for (int r0 = 0; r0 < S; r0 += kBigThreads) {  // uniform trip count
-      const int r = r0 + tid;
-      Geo g;
-      g.level = -1;
-      if (r < S) {
-        const ycx_cand b = ci[bucket[r]];
-        g = geometry(f32x4{b.x1, b.y1, b.x2, b.y2}, X0, Y0, inv, all_pairs);
-      }
-      for (int Lv = 0; Lv < kLevels; ++Lv) {
-        const bool in = g.level == Lv;
-        const unsigned long long m = __ballot(in);
-        if (!m) continue;
-        int mxw = in ? __float_as_int(g.w) : 0, mxh = in ? __float_as_int(g.h) : 0;
-        int mnw = in ? __float_as_int(g.w) : 0x7F800000, mnh = in ? __float_as_int(g.h) : 0x7F800000;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          mxw = max(mxw, __shfl_xor(mxw, o));
-          mxh = max(mxh, __shfl_xor(mxh, o));
-          mnw = min(mnw, __shfl_xor(mnw, o));
-          mnh = min(mnh, __shfl_xor(mnh, o));
-        }
-        if ((tid & 63) == 0) {
-          atomicAdd(&s_lv[Lv][0], __popcll(m));
-          atomicMax(&s_lv[Lv][1], mxw);
-          atomicMax(&s_lv[Lv][2], mxh);
-          atomicMin(&s_lv[Lv][3], mnw);
-          atomicMin(&s_lv[Lv][4], mnh);
-        }
-      }
-    }
-    __syncthreads();
-    if (tid < 64) wave_exclusive_scan(cells, cells, kCells);
-    __syncthreads();
-    // Boxes + u16 ranks + state in LDS when they fit (19 B per box), else the
-    // workspace (state still in LDS up to its size).
-    const bool lds = 19 * S + 32 <= kLdsBytes - kLdsCellBytes;
-    f32x4* lbox = reinterpret_cast<f32x4*>(smem + kLdsCellBytes);
-    unsigned short* lr = reinterpret_cast<unsigned short*>(smem + kLdsCellBytes + 16 * S);
-    unsigned char* st = lds ? reinterpret_cast<unsigned char*>(smem + kLdsCellBytes + 16 * S + ((2 * S + 15) & ~15))
-                            : S <= kLdsBytes - kLdsCellBytes ? reinterpret_cast<unsigned char*>(smem + kLdsCellBytes)
-                                                             : P.state + off;
-    for (int r = tid; r < S; r += kBigThreads) {
-      const int q = atomicAdd(&cells[P.nsup[off + r]], 1);  // cells[k] ends as the end of cell k
-      const ycx_cand b = ci[bucket[r]];
-      if (lds) {
-        lr[q] = (unsigned short)r;
-        lbox[q] = f32x4{b.x1, b.y1, b.x2, b.y2};
-      } else {
-        P.srank[off + q] = r;
-        P.sbox[off + q] = f32x4{b.x1, b.y1, b.x2, b.y2};
-      }
-    }
-    __syncthreads();
-    YCX_PROF_MARK(1)
-    const Frame fr{S, off, X0, Y0, inv, all_pairs};
-    if (lds) {
-      Ctx<true> c{cells, s_lv, lbox, lr, nullptr, t_lo, inv_t, S};
-      resolve<true>(c, fr, P, st, thr, &s_flag);
-    } else {
-      Ctx<false> c{cells, s_lv, P.sbox + off, nullptr, P.srank + off, t_lo, inv_t, S};
-      resolve<false>(c, fr, P, st, thr, &s_flag);
-    }
-#ifdef YCX_NMS_PROFILE
-    t_prev_ = __builtin_amdgcn_s_memtime();
-#endif
-    // (6) kept rows in rank order
-    int base = 0;
-    for (int r0 = 0; r0 < S; r0 += kBigThreads) {
-      const int r = r0 + tid;
-      const int k = (r < S && st[r] == 1) ? 1 : 0;
-      int total;
-      const int pos = block_exclusive(k, s_w, &total);
-      if (k) P.kept[off + base + pos] = bucket[r];
-      base += total;
-    }
-    if (tid == 0) P.kc[tk.cls] = base;
-    __syncthreads();
-    YCX_PROF_MARK(4)
-  }
-}
-
-// ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kThreads) nms_finish(ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws,
                                                        float* __restrict__ dets, int* __restrict__ keep_rows,
                                                        int* __restrict__ keep_counts) {
@@ -2113,14 +1948,9 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   // with the wide classes' sort + spatial index (nms_wide_a's work) in the same launch: at C4
   // the 24 wide and 24 fast classes of a batch then run side by side instead of in turn
   // (YCX_NMS_NO_FAST: every class on the wide path, the fast list empty)
-#ifdef YCX_NMS_OLD_BIG  // development A/B: the r02 general path for every class the fast path leaves
-  hipLaunchKernelGGL(nms_fast<8>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs, 0);
-  hipLaunchKernelGGL(nms_big, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs);
-#else
   hipLaunchKernelGGL(nms_fast<8>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs, 1);
   hipLaunchKernelGGL(nms_wide_s, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
   hipLaunchKernelGGL(nms_wide_b, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
-#endif
   hipLaunchKernelGGL(nms_finish, dim3(d->n), dim3(kThreads), 0, st, *d, cand, ws, dets, keep_rows, keep_counts);
   return ycx_launch_status();
 }
