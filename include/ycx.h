@@ -200,7 +200,8 @@ typedef struct ycx_head_desc {
 } ycx_head_desc;
 
 /* A pre-built op for ycx_run_ops (the static execution plan of Model.forward). */
-enum { YCX_OP_CONV = 1, YCX_OP_STEM = 2, YCX_OP_POOL = 3, YCX_OP_COPY = 4, YCX_OP_STEM2 = 5, YCX_OP_HEAD = 6 };
+enum { YCX_OP_CONV = 1, YCX_OP_STEM = 2, YCX_OP_POOL = 3, YCX_OP_COPY = 4, YCX_OP_STEM2 = 5, YCX_OP_HEAD = 6,
+       YCX_OP_CONV_PAIR = 7 };
 typedef struct ycx_op {
   int32_t kind;
   int32_t pad_;
@@ -208,7 +209,8 @@ typedef struct ycx_op {
     ycx_conv_desc conv;
     ycx_pool_desc pool;
     ycx_copy_desc copy;
-    ycx_conv_desc pair[2];  /* STEM2: [0] the stem, [1] the stride-2 conv it feeds */
+    ycx_conv_desc pair[2];  /* STEM2: [0] the stem, [1] the stride-2 conv it feeds;
+                               CONV_PAIR: [0] the first 1x1 conv, [1] the 1x1 conv reading it */
     struct {
       ycx_conv_desc conv;
       ycx_head_desc head;
@@ -219,12 +221,13 @@ typedef struct ycx_op {
   const float* bias;        /* bias (conv/stem; STEM2: the stem's)                  */
   void* out;                /* y                                                    */
   const void* residual;     /* optional residual (conv)                             */
-  const void* weight2;      /* STEM2: the second conv's packed bf16 weights         */
-  const float* bias2;       /* STEM2: the second conv's bias                        */
+  const void* weight2;      /* STEM2 / CONV_PAIR: the second conv's packed weights  */
+  const float* bias2;       /* STEM2 / CONV_PAIR: the second conv's bias            */
   void* cand;               /* HEAD: ycx_cand [n][rows_total]                      */
   int32_t* cand_rows;       /* HEAD: [n][rows_total]                                */
   int32_t* cand_counts;     /* HEAD: [n], zeroed before the first level's op        */
   int32_t* status;          /* HEAD (nullable): the range guard flag, below         */
+  void* out2;               /* CONV_PAIR: the second conv's output (out: the first's, nullable) */
 } ycx_op;
 
 int ycx_abi_version(void);
@@ -261,6 +264,16 @@ enum { YCX_HEAD_NONFINITE = 1 };
 ycx_status ycx_conv2d_head(const ycx_conv_desc* d, const ycx_head_desc* h, const void* x, const void* w,
                            const float* bias, float* heads, ycx_cand* cand, int32_t* cand_rows,
                            int32_t* cand_counts, int32_t* status, void* stream);
+/* Two chained 1x1 / stride-1 convs in one launch (Conv, nets/common.py:97-109, twice):
+ * ya = act_a(W_a x + b_a) (cin 64 / 128 / 256 -> cout 256, `ya` nullable: then it is
+ * not stored) and yb = act_b(W_b ya + b_b) (256 -> cout_pad 128 or 256), where `b` reads
+ * nothing but `a`'s output: the yolov7 160^2 ELAN exit (layer 11 -> layer 14,
+ * cfg/net/yolov7.yaml). The intermediate stays on chip (one HBM read of it saved);
+ * outputs bit-identical to two ycx_conv2d calls with the weight-resident 1x1 (tile 22).
+ * NHWC 16-bit (d->dtype bf16 / fp16), channel slices as ycx_conv2d. */
+ycx_status ycx_conv2d_pair(const ycx_conv_desc* a, const ycx_conv_desc* b, const void* x, const void* w_a,
+                           const float* bias_a, void* ya, const void* w_b, const float* bias_b, void* yb,
+                           void* stream);
 /* Stem conv: fp32 NCHW input (the model input, cin <= 4), weights fp32
  * [kh][kw][cin][cout_pad], output NHWC in d->dtype. in_c_* describe the NCHW
  * channel count (in_c_stride = channels of the input tensor). */

@@ -457,3 +457,74 @@ def test_stem_conv2_fused(device, stem_s, cout, act, nhw):
     got = t[5].cpu()
     assert torch.all(got[..., :out_extra] == 0)
     torch.testing.assert_close(got[..., out_extra:].permute(0, 3, 1, 2).double(), ref, rtol=2e-2, atol=2e-2)
+
+
+def _desc_1x1(n, h, w, cin, cout, cpad, in_off, in_stride, out_off, out_stride, act, dtype, tile=0):
+    d = L.ConvDesc()
+    d.n, d.h, d.w, d.cin, d.in_c_off, d.in_c_stride = n, h, w, cin, in_off, in_stride
+    d.ho, d.wo, d.cout, d.cout_pad, d.out_c_off, d.out_c_stride = h, w, cout, cpad, out_off, out_stride
+    d.kh = d.kw = 1
+    d.stride, d.pad, d.act, d.leaky_slope, d.dtype, d.out_layout, d.tile = 1, 0, act, 0.1, dtype, L.OUT_NHWC, tile
+    return d
+
+
+@pytest.mark.parametrize('dtype', [L.DT_BF16, L.DT_F16])
+@pytest.mark.parametrize('n,hw,cin,cout2,store1', [(2, (13, 11), 256, 128, True), (2, (13, 11), 64, 256, True),
+                                                   (1, (9, 7), 128, 120, False), (4, (128, 128), 256, 128, True),
+                                                   (3, (96, 80), 256, 256, False), (2, (64, 72), 128, 128, True)])
+def test_conv2d_pair(device, dtype, n, hw, cin, cout2, store1):
+    """ycx_conv2d_pair (tile 55): y1 = act(W1 x + b1) (cin -> 256) and y2 = act(W2 y1 + b2) in one
+    launch, against the same two convs run unfused with the weight-resident 1x1 (tile 22):
+    y1 and y2 bit-identical (same float operations in the same order), and against a float64
+    torch reference of the chain. Ragged pixel tails, several tiles per persistent block,
+    input / output channel slices, cout2 < cout_pad, y1 not stored."""
+    h, w = hw
+    tdt = torch.bfloat16 if dtype == L.DT_BF16 else torch.float16
+    g = torch.Generator().manual_seed(n * 7 + cin)
+    x = torch.randn(n, h, w, cin + 8, generator=g).to(tdt)
+    w1 = (torch.randn(256, cin, generator=g) / cin ** 0.5).to(tdt)
+    b1 = torch.randn(256, generator=g) * 0.1
+    cpad2 = 128 if cout2 <= 128 else 256
+    w2 = torch.zeros(cpad2, 256, dtype=tdt)
+    w2[:cout2] = (torch.randn(cout2, 256, generator=g) / 16.0).to(tdt)
+    b2 = torch.zeros(cpad2)
+    b2[:cout2] = torch.randn(cout2, generator=g) * 0.1
+    xd, w1d, b1d, w2d, b2d = [t.to(device) for t in (x, w1, b1, w2, b2)]
+    ya = torch.zeros(n, h, w, 256 + 16, dtype=tdt, device=device)
+    yb = torch.zeros(n, h, w, cout2 + 8, dtype=tdt, device=device)
+    da = _desc_1x1(n, h, w, cin, 256, 256, 8, cin + 8, 16, 272, L.ACT_SILU, dtype)
+    db = _desc_1x1(n, h, w, 256, cout2, cpad2, 16, 272, 8, cout2 + 8, L.ACT_LEAKY, dtype)
+    st = L.stream_handle(device)
+    L.check(L.lib.ycx_conv2d_pair(ctypes.byref(da), ctypes.byref(db), xd.data_ptr(), w1d.data_ptr(), b1d.data_ptr(),
+                                  ya.data_ptr() if store1 else None, w2d.data_ptr(), b2d.data_ptr(), yb.data_ptr(), st))
+    # unfused: the same two convs through ycx_conv2d, weight-resident 1x1 tiles
+    ya2, yb2 = torch.zeros_like(ya), torch.zeros_like(yb)
+    da.tile, db.tile = 22, 22
+    L.check(L.lib.ycx_conv2d(ctypes.byref(da), xd.data_ptr(), w1d.data_ptr(), b1d.data_ptr(), ya2.data_ptr(), None, st))
+    L.check(L.lib.ycx_conv2d(ctypes.byref(db), ya2.data_ptr(), w2d.data_ptr(), b2d.data_ptr(), yb2.data_ptr(), None, st))
+    torch.cuda.synchronize()
+    assert torch.equal(yb, yb2)
+    if store1:
+        assert torch.equal(ya, ya2)
+    else:
+        assert not ya.any()
+    assert not yb[..., :8].any() and not ya[..., :16].any()
+    mid = F.silu(x[..., 8:].double() @ w1.double().t() + b1.double())
+    ref = F.leaky_relu(mid.to(tdt).double() @ w2[:cout2].double().t() + b2[:cout2].double(), 0.1)
+    tol = 1e-2 if dtype == L.DT_BF16 else 2e-3
+    torch.testing.assert_close(yb[..., 8:].cpu().double(), ref, rtol=tol, atol=tol)
+
+
+def test_conv2d_pair_rejects(device):
+    """Tile 55 needs 1x1 / s1 pairs with cout_a = 256 (pad 256), cin_b = 256, cout_pad_b 128 / 256,
+    cin_a in {64, 128, 256} and 16-bit NHWC."""
+    t = torch.zeros(1 << 16, device=device)
+    ok = dict(a=(2, 8, 8, 128, 256, 256), b=(2, 8, 8, 256, 128, 128))
+    for a, b, dt in [((2, 8, 8, 128, 192, 256), ok['b'], L.DT_BF16), ((2, 8, 8, 96, 256, 256), ok['b'], L.DT_BF16),
+                     (ok['a'], (2, 8, 8, 256, 200, 256), L.DT_F32), (ok['a'], (2, 8, 8, 256, 384, 384), L.DT_BF16)]:
+        da = _desc_1x1(*a, 0, a[3], 0, a[4], L.ACT_SILU, dt)
+        db = _desc_1x1(*b, 0, b[3], 0, b[4], L.ACT_SILU, dt)
+        with pytest.raises(L.YcxError, match='unsupported|bad argument'):
+            L.check(L.lib.ycx_conv2d_pair(ctypes.byref(da), ctypes.byref(db), t.data_ptr(), t.data_ptr(),
+                                          t.data_ptr(), t.data_ptr(), t.data_ptr(), t.data_ptr(), t.data_ptr(),
+                                          L.stream_handle(device)))

@@ -147,12 +147,40 @@ def test_engine_plan_properties(device):
     # 95 convs minus the 3 folded RepConv 1x1 branches; at 640 the stem and layer 1 run fused (stem2)
     # and the 8 ELAN cv1/cv2 sibling pairs run as one conv each
     assert k.get('stem2', 0) == 1 and 'stem' not in k
-    assert sum(i.get('parts', 1) for i in eng.op_info if i['kind'] in ('conv', 'stem', 'stem2')) == 92
+    assert sum(i.get('parts', 1) for i in eng.op_info if i['kind'] in ('conv', 'stem', 'stem2', 'conv_pair')) == 92
+    # the 160^2 ELAN exit (layer 11 -> layer 14) runs as one fused 1x1 pair (tile 55) once the map
+    # gives the weight-resident kernel >= 8 tiles per CU (bs >= 6 at 640)
+    assert not any(i['kind'] == 'conv_pair' for i in eng.op_info)
+    eng8 = m.engine_for((8, 3, 640, 640), device, slot=7)
+    assert [i['shape'][1:5] for i in eng8.op_info if i['kind'] == 'conv_pair'] == [(160, 160, 256, 256)]
+    assert sum(i.get('parts', 1) for i in eng8.op_info if i['kind'] in ('conv', 'stem', 'stem2', 'conv_pair')) == 92
+    m.release_slot((8, 3, 640, 640), device, 7)
     assert sum(1 for i in eng.op_info if i['kind'] == 'conv' and i['parts'] == 2) == 8
     assert abs(s['gflop_per_image'] - 104.511078400) < 1e-6
     # the five MP k2 s2 pools run inside their 1x1 consumers; the SPPCSPC cascade is the one pool op
     assert sum(1 for i in eng.op_info if i['name'].endswith('+maxpool_k2s2')) == 5
     assert [i['name'] for i in eng.op_info if i['kind'] == 'pool'] == ['maxpool_k5s1_cascade3']
+
+
+def test_conv_pair_fusion_bit_identical(device, monkeypatch):
+    """The yolov7 plan with its 1x1 -> 1x1 chain fused (ycx_conv2d_pair) == the plan that runs
+    the two convs apart (YCX_NO_CONV_PAIR=1), bit for bit, in bf16 and fp16."""
+    from ycx.engine import Engine
+    for precision in ('bf16', 'fp16'):
+        m, _ = make_model('yolov7', 80, 0, precision)
+        m.to(device)
+        x = synthetic_images(8, 3, 640, 640, seed=6).to(device)
+        outs = []
+        for off in ('', '1'):
+            monkeypatch.setenv('YCX_NO_CONV_PAIR', off)
+            eng = Engine(m, tuple(x.shape), torch.device(device), precision)
+            try:
+                assert sum(1 for i in eng.op_info if i['kind'] == 'conv_pair') == (0 if off else 1)
+                outs.append([o.clone() for o in eng.run(x)])
+            finally:
+                eng.close()
+        for a, b in zip(*outs):
+            assert torch.equal(a, b)
 
 
 def test_pool_fusion_bit_identical(device):

@@ -2723,6 +2723,193 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
 }
 
 // -------------------------------------------------------------------------
+// Two chained 1x1 convs in one launch (tile 55, ycx_conv2d_pair): y1 = act(W1 x + b1)
+// (cin 64 KC -> 256) and y2 = act(W2 y1 + b2) (256 -> CO2), where the second conv reads
+// nothing but the first one's output (yolov7's 160^2 ELAN exit: layer 11, 256 -> 256,
+// feeding layer 14, 256 -> 128; layer 11's map also goes to the MP branch, so y1 is
+// still stored when the caller gives an output for it). conv1x1_wres's pipeline for
+// the first conv (eight waves, 32 output channels each, W1 rows resident in VGPRs,
+// 64-pixel tiles of x through the LDS-DMA ring); its epilogue also writes the
+// tile's bf16 y1 (64 pixels x 256 channels, the ring's swizzled slab layout) into
+// LDS, and after one barrier every wave runs the second conv on it with its own W2
+// rows in VGPRs (CO2 = 128: 32 channels x 32 pixels per wave; 256: 32 x 64). The
+// 64-pixel y1 tile never makes the HBM round trip of the unfused pair (at yolov7
+// bs 32: 419 MB less read). Both epilogues apply the same float operations as
+// conv1x1_wres's, so y1 and y2 are bit-identical to the two unfused launches.
+// The ring's counted vmcnt waits include both conversions' stores.
+// -------------------------------------------------------------------------
+template <int KC, int NS, int SUB, int CO2>
+__global__ void __launch_bounds__(512) conv1x1_wres_pair(ConvArgs a, ConvArgs b) {
+  constexpr int NW = 8, PT = 64, FM = 2, FN = 4, KS = KC / SUB, SLAB = PT * 128, STAGE = SUB * SLAB;
+  constexpr int A_PW = PT / (8 * NW);
+  constexpr int K2 = 256, FN2 = CO2 == 128 ? 2 : 4;  // second conv: K = 256, pixels per wave 16 FN2
+  static_assert(CO2 == 128 || CO2 == 256, "second conv: 128 or 256 output channels");
+  static_assert(KC % SUB == 0 && A_PW == 1, "slabs per stage");
+  constexpr int VM_RING = A_PW * SUB * (NS - 2);
+  constexpr int Y1_BYTES = (K2 / 64) * SLAB;  // y1 tile: 4 slabs of 64 pixels x 128 B
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE + Y1_BYTES];
+  char* const y1s = smem + NS * STAGE;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
+  const int R = a.nwg;
+  const int T = (a.M + PT - 1) / PT;
+  const int t0 = (int)((long long)L * T / R), t1 = (int)((long long)(L + 1) * T / R);
+  if (t0 >= t1) return;  // whole block: no barrier is left waiting
+  const int m16 = lane & 15;
+
+  // first conv: this wave's 32 output channels (rows permuted as conv1x1_wres)
+  const int cob = wid * 32;
+  const elt_t* __restrict__ W1 = reinterpret_cast<const elt_t*>(a.w);
+  eltx8 af[2 * KC][FM];
+#pragma unroll
+  for (int kq = 0; kq < 2 * KC; ++kq)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      af[kq][i] = *reinterpret_cast<const eltx8*>(W1 + (size_t)(cob + 8 * (m16 >> 2) + 4 * i + (m16 & 3)) * a.Ktot +
+                                                   32 * kq + 8 * (lane >> 4));
+  f32x4 bv[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) bv[i] = *reinterpret_cast<const f32x4*>(a.bias + cob + 8 * (lane >> 4) + 4 * i);
+  // second conv: channels cob2 .. +31, pixels 16 FN2 h2 .. of every tile
+  const int cob2 = CO2 == 128 ? (wid & 3) * 32 : wid * 32, h2 = CO2 == 128 ? wid >> 2 : 0;
+  const elt_t* __restrict__ W2 = reinterpret_cast<const elt_t*>(b.w);
+  eltx8 af2[K2 / 32][FM];
+#pragma unroll
+  for (int kq = 0; kq < K2 / 32; ++kq)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      af2[kq][i] = *reinterpret_cast<const eltx8*>(W2 + (size_t)(cob2 + 8 * (m16 >> 2) + 4 * i + (m16 & 3)) * b.Ktot +
+                                                    32 * kq + 8 * (lane >> 4));
+  f32x4 bv2[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int co = cob2 + 8 * (lane >> 4) + 4 * i;
+    bv2[i] = co < b.Cout ? *reinterpret_cast<const f32x4*>(b.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // LDS-DMA of x: wave-instruction wid fills rows 8 wid .. +7 of a slab
+  const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
+  const int x_bytes = a.M * a.in_cs * 2;
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int rrow = 8 * wid + lrow;
+  const int roff = (rrow * a.in_cs + a.in_coff + ((pch ^ swz<64>(rrow)) << 3)) * 2;
+  const int nst = (t1 - t0) * KS;
+  auto issue = [&](int s) {
+    const int tl = s / KS, ks = s - tl * KS;
+    const int px0 = (t0 + tl) * PT;
+    char* base = smem + (s % NS) * STAGE;
+#pragma unroll
+    for (int sb = 0; sb < SUB; ++sb) {
+      const int off = px0 + rrow < a.M ? px0 * a.in_cs * 2 + roff + (ks * SUB + sb) * 128 : 0x7FFFFFF0;
+      buf_lds16(X, x_bytes, off, 0, base + sb * SLAB + wid * 1024);
+    }
+  };
+  for (int s = 0; s < NS - 1 && s < nst; ++s) issue(s);
+
+  // every full tile stores exactly NSTO 16-byte vectors per wave (both outputs whole)
+  const bool store1 = a.y != nullptr;
+  constexpr int NSTO_MAX = FN + FN2;
+  const int nsto = (store1 ? FN : 0) + FN2;
+  const bool exact = b.Cout == b.Cout_pad;  // a.Cout == a.Cout_pad == 256 (host check)
+  elt_t* __restrict__ Y1 = store1 ? reinterpret_cast<elt_t*>(a.y) + a.out_coff : nullptr;
+  elt_t* __restrict__ Y2 = reinterpret_cast<elt_t*>(b.y) + b.out_coff;
+  int t = 0;
+  for (int tl = 0; tl < t1 - t0; ++tl) {
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks, ++t) {
+      if (t + NS - 2 >= nst) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      } else {
+        const int lo = t - NS + 1 > 0 ? t - NS + 1 : 0;  // tile ends: steps i KS + KS - 1
+        const int nb = exact && t >= KS ? (t - 1 - (KS - 1)) / KS - (lo + KS - 1 - (KS - 1)) / KS + 1 : 0;
+        if (exact) wait_vm_counted<VM_RING, 0, (NS + KS - 2) / KS * NSTO_MAX>(nb * nsto);
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + NS - 1 < nst) issue(t + NS - 1);
+      const char* B = smem + (t % NS) * STAGE;
+#pragma unroll
+      for (int kk = 0; kk < 2 * SUB; ++kk) {
+        const int c = (kk & 1) * 4 + (lane >> 4);
+        const char* Bs = B + (kk >> 1) * SLAB;
+        eltx8 bfr[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = j * 16 + (lane & 15);
+          bfr[j] = *reinterpret_cast<const eltx8*>(Bs + row * 128 + ((c ^ swz<64>(row)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = YCX_MFMA16(af[2 * SUB * ks + kk][i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // epilogue 1: y1 to HBM (when stored) and, as the second conv's B operand, to LDS.
+    // The previous tile's second-conv reads of y1s finished before this tile's ring barriers.
+    const int pt0 = (t0 + tl) * PT;
+    const int co = cob + 8 * (lane >> 4);  // channels co .. co+7
+    const int s1 = co >> 6, c1 = (co >> 3) & 7;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      eltx8 ov;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)ycx_act<true>(acc[i][j][q] + bv[i][q], a.act, a.slope);
+      const int row = j * 16 + (lane & 15), p = pt0 + row;
+      if (store1 && p < a.M)
+        if (YCX_OUT_OK(a, Y1 + (size_t)p * a.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y1 + (size_t)p * a.out_cs + co) = ov;
+      *reinterpret_cast<eltx8*>(y1s + s1 * SLAB + row * 128 + ((c1 ^ swz<64>(row)) << 4)) = ov;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the raw s_barrier does not wait for LDS stores
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // second conv on the y1 tile
+    f32x4 acc2[FM][FN2];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN2; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < K2 / 32; ++kk) {
+      const int c = (kk & 1) * 4 + (lane >> 4);
+      const char* Bs = y1s + (kk >> 1) * SLAB;
+      eltx8 bfr[FN2];
+#pragma unroll
+      for (int j = 0; j < FN2; ++j) {
+        const int row = h2 * 16 * FN2 + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const eltx8*>(Bs + row * 128 + ((c ^ swz<64>(row)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN2; ++j) acc2[i][j] = YCX_MFMA16(af2[kk][i], bfr[j], acc2[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int co2 = cob2 + 8 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < FN2; ++j) {
+      eltx8 ov;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)ycx_act<true>(acc2[i][j][q] + bv2[i][q], b.act, b.slope);
+      const int p = pt0 + h2 * 16 * FN2 + j * 16 + (lane & 15);
+      if (p < b.M && co2 < b.Cout)
+        if (YCX_OUT_OK(b, Y2 + (size_t)p * b.out_cs + co2, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y2 + (size_t)p * b.out_cs + co2) = ov;
+    }
+  }
+}
+
+// -------------------------------------------------------------------------
 // fp8 weight-resident 1x1 conv (tile 36): conv1x1_wres's structure on the
 // block-scaled e4m3 MFMA. Wave (wc, wp) holds the e4m3 rows of output channels
 // 32 wc .. +31 of its group for all of K in registers (K/4 VGPRs: 64 at
@@ -3077,6 +3264,7 @@ const TileInfo kTiles[] = {
     {64, 320, 64, "halo3x3_band_co64_8x40_s2"},
     {128, 160, 64, "halo3x3_band_co128_4x40_s2"},
     {128, 128, 64, "halo3x3s2_wsr_co128"},
+    {256, 64, 64, "wres1x1_pair"},  // 55: ycx_conv2d_pair only (two chained 1x1 convs)
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -3268,6 +3456,27 @@ ycx_status launch_wres(ConvArgs a, hipStream_t st) {
   return launch_wres_k<2, 4, 32, 6, 1>(a, st);
 }
 
+// tile 55: two chained 1x1 convs (conv1x1_wres_pair), one persistent block per CU
+template <int KC, int NS, int SUB>
+ycx_status launch_wres_pair_k(ConvArgs a, ConvArgs b, hipStream_t st) {
+  const int T = (a.M + 63) / 64;
+  a.nwg = std::max(1, std::min(T, 256));
+  if (b.Cout_pad == 128)
+    hipLaunchKernelGGL((conv1x1_wres_pair<KC, NS, SUB, 128>), dim3(a.nwg), dim3(512), 0, st, a, b);
+  else
+    hipLaunchKernelGGL((conv1x1_wres_pair<KC, NS, SUB, 256>), dim3(a.nwg), dim3(512), 0, st, a, b);
+  return ycx_launch_status();
+}
+
+ycx_status launch_wres_pair(ConvArgs a, ConvArgs b, hipStream_t st) {
+  switch (a.Cin) {
+    case 64: return launch_wres_pair_k<1, 5, 1>(a, b, st);
+    case 128: return launch_wres_pair_k<2, 5, 2>(a, b, st);
+    case 256: return launch_wres_pair_k<4, YCX_WRES_NS, 2>(a, b, st);
+    default: return YCX_ERR_UNSUPPORTED;
+  }
+}
+
 bool wres_f8_ok(const ConvArgs& a) {
   return a.KH == 1 && a.KW == 1 && a.S == 1 && a.P == 0 && a.H == a.Ho && a.W == a.Wo && !a.res &&
          a.out_layout == YCX_OUT_NHWC && (a.Cin == 128 || a.Cin == 256 || a.Cin == 512) && a.Ktot == a.Cin &&
@@ -3440,6 +3649,8 @@ extern "C" ycx_status ycx_conv2d_head_f16(const ycx_conv_desc*, const ycx_head_d
                                           const float*, float*, ycx_cand*, int32_t*, int32_t*, int32_t*, void*);
 extern "C" ycx_status ycx_stem_conv_f16(const ycx_conv_desc*, const float*, const float*, const float*, void*,
                                         void*);
+extern "C" ycx_status ycx_conv2d_pair_f16(const ycx_conv_desc*, const ycx_conv_desc*, const void*, const void*,
+                                          const float*, void*, const void*, const float*, void*, void*);
 extern "C" ycx_status ycx_stem_conv2_f16(const ycx_conv_desc*, const ycx_conv_desc*, const float*, const float*,
                                          const float*, const void*, const float*, void*, void*);
 #define YCX_TO_F16(cond, call) \
@@ -3574,6 +3785,33 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d_head)(const ycx_conv_desc* d, const ycx
   a.out_cs = d->cout;
   HeadArgs hd{*h, cand, cand_rows, cand_counts, heads, status};
   return launch_head(a, hd, reinterpret_cast<hipStream_t>(stream), f8);
+}
+
+extern "C" ycx_status YCX_SFX(ycx_conv2d_pair)(const ycx_conv_desc* da, const ycx_conv_desc* db, const void* x,
+                                               const void* wa, const float* ba, void* ya, const void* wb,
+                                               const float* bb, void* yb, void* stream) {
+  YCX_TO_F16(da && da->dtype == YCX_DT_F16,
+             ycx_conv2d_pair_f16(da, db, x, wa, ba, ya, wb, bb, yb, stream));
+  YCX_CHECK_ARG(da && db && x && wa && ba && wb && bb && yb);
+  YCX_CHECK_ARG(da->n > 0 && da->h > 0 && da->w > 0 && da->cin > 0 && da->cout > 0);
+  YCX_CHECK_ARG(da->ho == da->h && da->wo == da->w && db->n == da->n && db->h == da->ho && db->w == da->wo &&
+                db->ho == db->h && db->wo == db->w && db->cin == da->cout && db->cout > 0);
+  YCX_CHECK_ARG(da->in_c_off >= 0 && da->in_c_off + da->cin <= da->in_c_stride && db->cout_pad >= db->cout);
+  YCX_CHECK_ARG(db->out_c_off >= 0 && db->out_c_off + db->cout <= db->out_c_stride);
+  YCX_CHECK_ARG(!ya || (da->out_c_off >= 0 && da->out_c_off + da->cout <= da->out_c_stride));
+  YCX_CHECK_SUPPORTED(da->dtype == YCX_DT_ELT && db->dtype == YCX_DT_ELT);
+  for (const ycx_conv_desc* d : {da, db}) {
+    YCX_CHECK_SUPPORTED(d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && !d->in_pool &&
+                        d->out_layout == YCX_OUT_NHWC && d->act >= YCX_ACT_NONE && d->act <= YCX_ACT_LEAKY);
+    YCX_CHECK_SUPPORTED(d->out_c_off % 8 == 0 && d->out_c_stride % 8 == 0);
+  }
+  YCX_CHECK_SUPPORTED((da->cin == 64 || da->cin == 128 || da->cin == 256) && da->cout == 256 && da->cout_pad == 256);
+  YCX_CHECK_SUPPORTED(da->in_c_off % 8 == 0 && da->in_c_stride % 8 == 0);
+  YCX_CHECK_SUPPORTED(db->cin == 256 && (db->cout_pad == 128 || db->cout_pad == 256) && db->cout % 8 == 0);
+  YCX_CHECK_SUPPORTED((long long)da->n * da->h * da->w * da->in_c_stride * 2 < (1LL << 31) - 64);
+  ConvArgs a = make_args(da, x, wa, ba, ya, nullptr);
+  ConvArgs b = make_args(db, nullptr, wb, bb, yb, nullptr);
+  return launch_wres_pair(a, b, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" ycx_status YCX_SFX(ycx_stem_conv)(const ycx_conv_desc* d, const float* x, const float* w,

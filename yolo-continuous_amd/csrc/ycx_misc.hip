@@ -432,6 +432,9 @@ static ycx_status run_one(const ycx_op& op, void* stream) {
     case YCX_OP_STEM2:
       return ycx_stem_conv2(&op.d.pair[0], &op.d.pair[1], (const float*)op.in, (const float*)op.weight, op.bias,
                             op.weight2, op.bias2, op.out, stream);
+    case YCX_OP_CONV_PAIR:
+      return ycx_conv2d_pair(&op.d.pair[0], &op.d.pair[1], op.in, op.weight, op.bias, op.out, op.weight2, op.bias2,
+                             op.out2, stream);
     case YCX_OP_HEAD:
       return ycx_conv2d_head(&op.d.head.conv, &op.d.head.head, op.in, op.weight, op.bias, (float*)op.out,
                              (ycx_cand*)op.cand, op.cand_rows, op.cand_counts, op.status, stream);
@@ -470,11 +473,13 @@ extern "C" ycx_status ycx_set_trace(int32_t on) {
 }
 
 static void trace_push(int32_t i, const ycx_op& op) {
-  static const char* kinds[] = {"?", "conv", "stem", "pool", "copy", "stem2", "head"};
-  const char* k = (op.kind >= 1 && op.kind <= 6) ? kinds[op.kind] : kinds[0];
+  static const char* kinds[] = {"?", "conv", "stem", "pool", "copy", "stem2", "head", "conv_pair"};
+  const char* k = (op.kind >= 1 && op.kind <= 7) ? kinds[op.kind] : kinds[0];
   char buf[160];
-  if (op.kind == YCX_OP_CONV || op.kind == YCX_OP_STEM || op.kind == YCX_OP_HEAD || op.kind == YCX_OP_STEM2) {
-    const ycx_conv_desc& c = op.kind == YCX_OP_HEAD ? op.d.head.conv : op.kind == YCX_OP_STEM2 ? op.d.pair[1] : op.d.conv;
+  if (op.kind == YCX_OP_CONV || op.kind == YCX_OP_STEM || op.kind == YCX_OP_HEAD || op.kind == YCX_OP_STEM2 ||
+      op.kind == YCX_OP_CONV_PAIR) {
+    const ycx_conv_desc& c = op.kind == YCX_OP_HEAD ? op.d.head.conv
+                             : op.kind == YCX_OP_STEM2 || op.kind == YCX_OP_CONV_PAIR ? op.d.pair[1] : op.d.conv;
     snprintf(buf, sizeof buf, "op%d %s %s n%d %dx%d %d->%d k%d s%d", i, k,
              op.kind == YCX_OP_CONV ? ycx_conv_tile_name(c.tile ? c.tile : ycx_conv_pick_tile(&c)) : "", c.n, c.h,
              c.w, c.cin, c.cout, c.kh, c.stride);

@@ -25,7 +25,7 @@ YCX_OK, YCX_ERR_BAD_ARG, YCX_ERR_UNSUPPORTED, YCX_ERR_LAUNCH, YCX_ERR_CAPACITY =
 DT_BF16, DT_F32, DT_FP8, DT_F16 = 0, 1, 2, 3
 ACT_NONE, ACT_SILU, ACT_LEAKY = 0, 1, 2
 OUT_NHWC, OUT_NCHW_F32, OUT_NHWC_UP2 = 0, 1, 2
-OP_CONV, OP_STEM, OP_POOL, OP_COPY, OP_STEM2, OP_HEAD = 1, 2, 3, 4, 5, 6
+OP_CONV, OP_STEM, OP_POOL, OP_COPY, OP_STEM2, OP_HEAD, OP_CONV_PAIR = 1, 2, 3, 4, 5, 6, 7
 
 _i32 = ctypes.c_int32
 
@@ -97,7 +97,7 @@ class Op(ctypes.Structure):
                 ("out", ctypes.c_void_p), ("residual", ctypes.c_void_p),
                 ("weight2", ctypes.c_void_p), ("bias2", ctypes.c_void_p),
                 ("cand", ctypes.c_void_p), ("cand_rows", ctypes.c_void_p), ("cand_counts", ctypes.c_void_p),
-                ("status", ctypes.c_void_p)]
+                ("status", ctypes.c_void_p), ("out2", ctypes.c_void_p)]
 
 
 class LetterboxDesc(ctypes.Structure):
@@ -131,6 +131,8 @@ _SIGS = [
     ("ycx_correct_boxes", _i32, [ctypes.POINTER(CorrectDesc), _VP, _VP, _VP, _VP]),
     ("ycx_stem_conv2", _i32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP,
                               _VP]),
+    ("ycx_conv2d_pair", _i32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP,
+                               _VP, _VP]),
     ("ycx_maxpool", _i32, [ctypes.POINTER(PoolDesc), _VP, _VP, _VP]),
     ("ycx_copy_channels", _i32, [ctypes.POINTER(CopyDesc), _VP, _VP, _VP]),
     ("ycx_quantize_fp8", _i32, [_VP, _VP, ctypes.c_int64, ctypes.c_float, _VP]),

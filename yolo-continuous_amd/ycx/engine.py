@@ -563,6 +563,65 @@ class Engine:
             pairs[id(nd)] = c
         return pairs
 
+    def _conv_pairs(self, pooled):
+        """1x1 -> 1x1 chains that run as one ycx_conv2d_pair launch (tile 55): a 1x1 / s1
+        conv with cin 64 / 128 / 256 and 256 output channels on a map large enough for the
+        weight-resident kernel (>= 8 64-pixel tiles per CU), whose output a second 1x1 / s1
+        conv (cin 256, cout_pad 128 / 256) reads directly; the first conv's output is still
+        stored when anything else reads it (yolov7: layer 11 -> layer 14 at 160^2, layer 11
+        also feeding the MP branch). 16-bit plans; YCX_NO_CONV_PAIR=1 keeps them apart.
+        Returns {id(first conv): second conv}."""
+        out = {}
+        if not self.h16 or os.environ.get('YCX_NO_CONV_PAIR'):
+            return out
+        taken = set()
+
+        def pointwise(nd):
+            q = nd.p
+            return (nd.kind == 'conv' and q['k'] == 1 and q['s'] == 1 and q['p'] == 0 and q['residual'] is None and
+                    q['layout'] == L.OUT_NHWC and id(nd) not in pooled)
+
+        for a in self.graph.nodes:
+            if not pointwise(a) or id(a) in taken:
+                continue
+            x, v = a.inputs[0], a.out
+            cin, cout = int(a.p['w'].shape[1]), int(a.p['w'].shape[0])
+            if cin not in (64, 128, 256) or cout != 256 or v.role != 'act' or v.buf is None:
+                continue
+            if x.n * x.h * x.w < 8 * 64 * 256 or (x.role != 'input' and (x.coff % 8 or x.buf.c % 8)):
+                continue
+            for b in v.consumers:
+                if not pointwise(b) or b.inputs[0] is not v or id(b) in taken or id(b) in out:
+                    continue
+                cb = int(b.p['w'].shape[0])
+                if self._cout_pad(cb) not in (128, 256) or cb % 8:
+                    continue
+                out[id(a)] = b
+                taken.update((id(a), id(b)))
+                break
+        return out
+
+    def _pair_op(self, a, b):
+        """One OP_CONV_PAIR for the chain a -> b (``_conv_pairs``)."""
+        da, wa, ba, fa, shape = self._conv_parts(a)
+        db, wb, bb, fb, _ = self._conv_parts(b)
+        op = L.Op()
+        op.kind = L.OP_CONV_PAIR
+        op.d.pair[0], op.d.pair[1] = da, db
+        idx = len(self.op_info)
+        v = a.out
+        store_a = len(v.consumers) > 1
+        op.in_ = self._val_ptr(a.inputs[0], idx, 'in_')
+        op.weight, op.bias = wa.data_ptr(), ba.data_ptr()
+        op.weight2, op.bias2 = wb.data_ptr(), bb.data_ptr()
+        op.out = self._val_ptr(v, idx, 'out') if store_a else None
+        op.out2 = self._val_ptr(b.out, idx, 'out2')
+        nbytes = (self._conv_bytes(da, wa, out_bytes=store_a) +
+                  self._conv_bytes(db, wb) - db.n * db.h * db.w * db.cin * self.dtype.itemsize)  # y1 stays on chip
+        self.op_info.append(dict(kind='conv_pair', name='wres1x1_pair', flops=fa + fb, shape=shape, parts=2,
+                                 shape2=(db.n, db.h, db.w, db.cin, db.cout, 1, 1), bytes=nbytes))
+        return op
+
     def _build(self):
         dev, dt = self.device, self.dtype
         self.buffers, self.params = [], []
@@ -578,12 +637,16 @@ class Engine:
             fused.update(id(nd) for nd in c[1:])
         pooled = self._pool_convs()  # {id(conv): pool node} (the pool runs inside the conv)
         fused.update(id(nd) for nd in pooled.values())
+        chains = self._conv_pairs(pooled)  # {id(first 1x1): second 1x1} (one launch each)
+        fused.update(id(nd) for nd in chains.values())
         for node in self.graph.nodes:
             k = node.kind
             if id(node) in fused:
                 continue
             if id(node) in pairs:
                 ops.append(self._stem2_op(node, pairs[id(node)]))
+            elif id(node) in chains:
+                ops.append(self._pair_op(node, chains[id(node)]))
             elif k in ('conv', 'stem'):
                 ops.append(self._conv_op(node, pool=pooled.get(id(node))))
             elif k == 'pool':

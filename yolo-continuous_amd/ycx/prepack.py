@@ -27,7 +27,7 @@ import json
 
 import torch
 
-FORMAT = "ycx-prepack-1"
+FORMAT = "ycx-prepack-2"  # 2 (r04): fused 1x1 pairs pack their two weight sets back to back
 
 
 def state_dict_sha256(model):
