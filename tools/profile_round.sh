@@ -1,20 +1,32 @@
 #!/bin/bash
-# Profile this round's bench on the GPU box (run through gpurun):
-#   bash tools/profile_round.sh r01
-# 1. rocprofv3 --kernel-trace --stats of the default bench command
-# 2. two PMC passes (FETCH_SIZE, WRITE_SIZE) over tools/pmc_workload.py
-# 3. tools/pmc_traffic.py -> per-op HBM bytes (traffic.json)
-# 4. the bench again, now reporting roofline.traffic from traffic.json
-# Everything lands in gpurun_out/<round>/; copy the summaries into profiles/<round>/.
+# Profile this round's bench on the GPU box (run through gpurun), one coherent set from one build:
+#   bash tools/profile_round.sh r04
+# 1. rocprofv3 --kernel-trace --stats of the default bench command; the same run writes the per-op
+#    roofline gap table (YCX_BENCH_KERNELS, HIP events of the serial roofline leg)
+# 2. tools/trace_leg_stats.py: the profiler's own per-kernel averages over that roofline leg
+# 3. two PMC passes (FETCH_SIZE, WRITE_SIZE) over tools/pmc_workload.py
+# 4. tools/pmc_traffic.py -> per-op HBM bytes (traffic.json)
+# 5. the bench again, now reporting roofline.traffic from profiles/<round>/traffic.json
+# Everything lands in gpurun_out/<round>/ and the summaries are copied to profiles/<round>/.
 set -e -o pipefail
-R=${1:-r01}
+R=${1:-r04}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/gpurun_out/$R
-mkdir -p "$OUT" "$ROOT/profiles/$R"
+P=$ROOT/profiles/$R
+mkdir -p "$OUT" "$P"
 cd /tmp
 export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
-  python3 "$ROOT/bench.py" > "$OUT/bench_under_rocprof.log" 2>&1
+YCX_BENCH_KERNELS=$OUT/ops.json timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run \
+  --output-format csv -- python3 "$ROOT/bench.py" > "$OUT/bench_under_rocprof.log" 2>&1
+tail -n 1 "$OUT/bench_under_rocprof.log" > "$P/bench_under_rocprof.json"
+STATS=$(find "$OUT/trace" -name '*kernel_stats.csv' | head -n 1)
+TRACE=$(find "$OUT/trace" -name '*kernel_trace.csv' | head -n 1)
+cp "$STATS" "$P/kernel_stats.csv"
+NOPS=$(python3 -c "import json; print(len(json.load(open('$OUT/ops.json'))['ops']))")
+python3 "$ROOT/tools/trace_leg_stats.py" "$TRACE" "$NOPS" 3 "$P/kernel_stats_roofline_leg.csv" > "$OUT/trace_legs.txt"
+cp "$OUT/trace_legs.txt" "$P/trace_legs.txt"
+cp "$OUT/ops.json" "$P/ops.json"
+python3 "$ROOT/tools/op_gap.py" "$OUT/ops.json" > "$P/op_gap.md"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
   python3 "$ROOT/tools/pmc_workload.py" > "$OUT/pmc_fetch.log" 2>&1
 cp "$ROOT/gpurun_out/pmc_ops.json" "$OUT/pmc_ops_fetch.json"
@@ -22,7 +34,9 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output
   python3 "$ROOT/tools/pmc_workload.py" > "$OUT/pmc_write.log" 2>&1
 python3 "$ROOT/tools/pmc_traffic.py" --fetch "$OUT/pmc_fetch" --write "$OUT/pmc_write" \
   --ops "$ROOT/gpurun_out/pmc_ops.json" --out "$OUT/traffic.json" > "$OUT/traffic_summary.json"
-cp "$OUT/traffic.json" "$ROOT/profiles/$R/traffic.json"
+cp "$OUT/traffic.json" "$P/traffic.json"
+cp "$OUT/traffic_summary.json" "$P/traffic_summary.json"
 cd "$ROOT"
 timeout -k 10 300 python3 bench.py > "$OUT/bench.log" 2>&1
-tail -n 1 "$OUT/bench.log"
+tail -n 1 "$OUT/bench.log" > "$P/bench.json"
+tail -n 1 "$OUT/bench.log" | cut -c1-600
