@@ -18,7 +18,12 @@ def main(path, top=None):
     print(f"# Per-op roofline gaps — {d.get('precision')} {d.get('shape')}\n")
     print(f"Peaks: {d.get('peak_tflops')} TFLOP/s MFMA, {d.get('hbm_peak_gbs')} GB/s HBM. "
           f"Forward {d['forward_kernel_ms']:.3f} ms, floor {d['forward_floor_ms']:.3f} ms, "
-          f"gap {d['forward_gap_ms']:.3f} ms.\n")
+          f"gap {d['forward_gap_ms']:.3f} ms.")
+    if d.get('forward_graph_ms'):
+        print(f"Per-op times: HIP events around every op of serial forwards ({d['forward_events_ms']:.3f} ms in all), "
+              f"less the event-record overhead spread evenly, so that they sum to the HIP-graph replay forward "
+              f"({d['forward_graph_ms']:.3f} ms).")
+    print()
     by = {}
     for o in ops:
         s = by.setdefault(o['bound'], [0.0, 0.0, 0])

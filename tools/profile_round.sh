@@ -7,26 +7,21 @@
 # 3. two PMC passes (FETCH_SIZE, WRITE_SIZE) over tools/pmc_workload.py
 # 4. tools/pmc_traffic.py -> per-op HBM bytes (traffic.json)
 # 5. the bench again, now reporting roofline.traffic from profiles/<round>/traffic.json
-# Everything lands in gpurun_out/<round>/ and the summaries are copied to profiles/<round>/.
+# Everything lands in gpurun_out/<round>/ (the box merges only gpurun_out/ back); then, locally,
+#   bash tools/collect_profile.sh r04   copies the summaries into profiles/<round>/.
 set -e -o pipefail
 R=${1:-r04}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/gpurun_out/$R
-P=$ROOT/profiles/$R
-mkdir -p "$OUT" "$P"
+mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 YCX_BENCH_KERNELS=$OUT/ops.json timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run \
   --output-format csv -- python3 "$ROOT/bench.py" > "$OUT/bench_under_rocprof.log" 2>&1
-tail -n 1 "$OUT/bench_under_rocprof.log" > "$P/bench_under_rocprof.json"
-STATS=$(find "$OUT/trace" -name '*kernel_stats.csv' | head -n 1)
 TRACE=$(find "$OUT/trace" -name '*kernel_trace.csv' | head -n 1)
-cp "$STATS" "$P/kernel_stats.csv"
 NOPS=$(python3 -c "import json; print(len(json.load(open('$OUT/ops.json'))['ops']))")
-python3 "$ROOT/tools/trace_leg_stats.py" "$TRACE" "$NOPS" 3 "$P/kernel_stats_roofline_leg.csv" > "$OUT/trace_legs.txt"
-cp "$OUT/trace_legs.txt" "$P/trace_legs.txt"
-cp "$OUT/ops.json" "$P/ops.json"
-python3 "$ROOT/tools/op_gap.py" "$OUT/ops.json" > "$P/op_gap.md"
+python3 "$ROOT/tools/trace_leg_stats.py" "$TRACE" "$NOPS" 3 "$OUT/kernel_stats_roofline_leg.csv" > "$OUT/trace_legs.txt"
+python3 "$ROOT/tools/op_gap.py" "$OUT/ops.json" > "$OUT/op_gap.md"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
   python3 "$ROOT/tools/pmc_workload.py" > "$OUT/pmc_fetch.log" 2>&1
 cp "$ROOT/gpurun_out/pmc_ops.json" "$OUT/pmc_ops_fetch.json"
@@ -34,9 +29,7 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output
   python3 "$ROOT/tools/pmc_workload.py" > "$OUT/pmc_write.log" 2>&1
 python3 "$ROOT/tools/pmc_traffic.py" --fetch "$OUT/pmc_fetch" --write "$OUT/pmc_write" \
   --ops "$ROOT/gpurun_out/pmc_ops.json" --out "$OUT/traffic.json" > "$OUT/traffic_summary.json"
-cp "$OUT/traffic.json" "$P/traffic.json"
-cp "$OUT/traffic_summary.json" "$P/traffic_summary.json"
+mkdir -p "$ROOT/profiles/$R" && cp "$OUT/traffic.json" "$ROOT/profiles/$R/traffic.json"  # read by the bench below
 cd "$ROOT"
 timeout -k 10 300 python3 bench.py > "$OUT/bench.log" 2>&1
-tail -n 1 "$OUT/bench.log" > "$P/bench.json"
 tail -n 1 "$OUT/bench.log" | cut -c1-600
