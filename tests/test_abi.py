@@ -38,6 +38,11 @@ def test_abi_metadata_without_gpu():
     assert _lib.lib.ycx_struct_size(99) == 0
     assert b"bad argument" in _lib.lib.ycx_strerror(1)
     assert _lib.lib.ycx_conv_tile_name(1) == b"bf16_co128_px128_k64"
+    # tile ids are positions in the library's table: retired ids keep placeholders
+    assert _lib.lib.ycx_conv_tile_name(16) == b"glds_co128_px128_k64_s2"
+    assert _lib.lib.ycx_conv_tile_name(50) == b"halo3x3s2_wsr_co128"
+    assert _lib.lib.ycx_conv_tile_name(55) == b"wres1x1_pair"
+    assert _lib.lib.ycx_conv_tile_name(56) == b"invalid"
     # argument validation happens before any device call
     assert _lib.lib.ycx_conv2d(None, None, None, None, None, None, None) == _lib.YCX_ERR_BAD_ARG
     assert _lib.lib.ycx_sort_nms(None, None, None, None, None, 0, None, None, None, None) == _lib.YCX_ERR_BAD_ARG

@@ -3264,6 +3264,10 @@ const TileInfo kTiles[] = {
     {64, 320, 64, "halo3x3_band_co64_8x40_s2"},
     {128, 160, 64, "halo3x3_band_co128_4x40_s2"},
     {128, 128, 64, "halo3x3s2_wsr_co128"},
+    {256, 128, 64, "retired_glds16w_co256_px128_s2"},  // 51-54: 16-wave tiles, measured slower
+    {128, 256, 64, "retired_glds16w_co128_px256_s2"},
+    {256, 128, 64, "retired_glds16w_co256_px128_s3"},
+    {128, 256, 64, "retired_glds16w_co128_px256_s3"},
     {256, 64, 64, "wres1x1_pair"},  // 55: ycx_conv2d_pair only (two chained 1x1 convs)
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
