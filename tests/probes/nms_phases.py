@@ -61,7 +61,8 @@ def main():
     wt = buf[16 + 7]
     if wt:
         print(f"  nms_wide: {wt // reps} tasks/step; " + "  ".join(
-            f"{n} {buf[16 + i] / wt / 1e3:.1f}" for i, n in enumerate(PHASES)) + f" kcycles/task; rounds/task {buf[21] / wt:.1f}")
+            f"{n} {buf[16 + i] / wt / 1e3:.1f}" for i, n in enumerate(PHASES)) + f" kcycles/task; rounds/task {buf[21] / wt:.1f}; "
+              f"positions visited in rounds/task {buf[22] / wt:.0f}")
     cnt = det.counts.cpu()
     print("candidates/img", cnt.float().mean().item())
     ws = det.ws.view(torch.int32).cpu()  # header (ntasks) then the task table {img, cls, off, S} at byte 256

@@ -486,6 +486,16 @@ def test_nms_spatial_wide_sizes(device, thr, rows):
     _check_keep(_random_pred(2, rows, 2, seed=11), 2, 0.0, thr)
 
 
+def test_nms_many_big_classes_unsplit(device):
+    """More big classes per batch than the split threshold (64): the fast classes then run
+    whole on a workgroup each inside nms_fast (the C2 regime), beside one wide class whose
+    search and fixed point run in nms_search / nms_resolve. Every other big-class test here
+    has few classes and takes the split path."""
+    pred = _random_pred(2, 40000, 40, seed=18, size_lo=-2.5, size_hi=-1.0)  # ~1000 rows per class
+    pred[0, :9000, 5] = 2.0  # class 0 of image 0: ~9.5k rows, past the LDS-resident size
+    _check_keep(pred, 40, 0.0, 0.45)
+
+
 def test_nms_spatial_pixel_coords_and_clusters(device):
     # pixel units (class extent normalisation) and tight clusters of near-duplicates
     pred = _random_pred(1, 5000, 1, seed=12, scale=640.0, size_lo=-2.5, size_hi=-0.5)

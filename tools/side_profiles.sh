@@ -1,16 +1,24 @@
 #!/bin/bash
-# Kernel-trace summaries of the side configurations (run through gpurun):
-#   bash tools/side_profiles.sh r02  ->  gpurun_out/<round>/side_prof_{fp8_b64,c4_1280}/
+# Side configurations of BASELINE.json under rocprofv3 --kernel-trace --stats, each with its bench
+# line and per-op roofline gap table (run through gpurun):
+#   bash tools/side_profiles.sh r04  ->  gpurun_out/<round>/side_<name>/ + side_<name>.json / _ops.json
+# fp16 bs 32 (the north_star mode), fp8 bs 64 (C5), 1280^2 bs 8 (C4), bf16 bs 64 (C5's shape in bf16).
 set -e -o pipefail
-R=${1:-r02}
+R=${1:-r04}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/gpurun_out/$R
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/side_prof_fp8_b64" -o run --output-format csv -- \
-  python3 "$ROOT/bench.py" --precision fp8 --batch 64 --cpu-seconds 0 --steps 40 > "$OUT/side_prof_fp8_b64.log" 2>&1
-tail -n 1 "$OUT/side_prof_fp8_b64.log" | cut -c1-200
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/side_prof_c4_1280" -o run --output-format csv -- \
-  python3 "$ROOT/bench.py" --size 1280 --batch 8 --cpu-seconds 0 --steps 40 > "$OUT/side_prof_c4_1280.log" 2>&1
-tail -n 1 "$OUT/side_prof_c4_1280.log" | cut -c1-200
+run() {  # name, bench args...
+  local name=$1; shift
+  YCX_BENCH_KERNELS=$OUT/side_${name}_ops.json timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+    -d "$OUT/side_$name" -o run --output-format csv -- python3 "$ROOT/bench.py" --cpu-seconds 0 --steps 40 "$@" \
+    > "$OUT/side_$name.log" 2>&1
+  grep '^{"metric' "$OUT/side_$name.log" | tail -n 1 > "$OUT/side_$name.json"
+  cut -c1-160 "$OUT/side_$name.json"
+}
+run fp16 --precision fp16
+run fp8_b64 --precision fp8 --batch 64
+run c4_1280 --size 1280 --batch 8
+run b64 --batch 64

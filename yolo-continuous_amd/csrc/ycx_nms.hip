@@ -97,15 +97,26 @@ constexpr int kPrepB = 16;  // workgroups per image in the class bucketing (nms_
 // G3 load 24.0k -> 58.9k img/s decode + NMS; C2 neutral; C4 +1.3 %; 16: C2 post 0.51 -> 0.57 ms)
 constexpr int kPrepClsB = YCX_PREP_CLS_B;
 
+// Big classes per batch (fast + wide lists) up to which the fast classes are split too: their
+// sort + spatial index stay in nms_fast, their suppressor search joins the wide classes' in
+// nms_search (positions spread evenly over the grid) and their fixed point runs in nms_resolve.
+// Past it (C2: ~160 fast classes per batch) every fast class already has a CU of its own for
+// its whole life and runs unsplit (a split at that load cost 7 %).
+#ifndef YCX_NMS_SPLIT_TASKS
+#define YCX_NMS_SPLIT_TASKS 64
+#endif
+constexpr int kSplitTasks = YCX_NMS_SPLIT_TASKS;
+
 struct Layout {
-  size_t hdr, tasks, wframes, wcells, bcnt, per_image_base;  // header + task tables + wide-class index +
-                                                             // slice class counts (batch), then per image:
+  size_t hdr, tasks, wframes, wcells, fframes, fcells, bcnt, per_image_base;  // header + task tables +
+                                  // wide / split-fast class indexes + slice class counts (batch), then per image:
   size_t keys, bucket, kept, sbox, srank, nsup, slots, state, cnt, offs, kc, per_image;
   int max_tasks, max_wide;  // big classes per image; wide classes per image
 };
 
 __host__ __device__ inline int wide_min_s();  // the smallest class the wide path can get
 __host__ __device__ inline size_t wide_cells_bytes();
+__host__ __device__ inline size_t fast_cells_bytes();
 struct WFrame;  // per wide class: extent normalisation, level stats (nms_wide_a -> _s, _b)
 __host__ __device__ inline size_t wframe_bytes();
 
@@ -125,7 +136,9 @@ __host__ __device__ inline Layout layout(int n, int rows) {
   L.max_wide = rows / wide_min_s() + 1;
   L.wframes = al(L.tasks + 2 * (size_t)n * L.max_tasks * sizeof(Task));  // fast list, then wide list
   L.wcells = al(L.wframes + (size_t)n * L.max_wide * wframe_bytes());
-  L.bcnt = al(L.wcells + (size_t)n * L.max_wide * wide_cells_bytes());
+  L.fframes = al(L.wcells + (size_t)n * L.max_wide * wide_cells_bytes());
+  L.fcells = al(L.fframes + (size_t)kSplitTasks * wframe_bytes());
+  L.bcnt = al(L.fcells + (size_t)kSplitTasks * fast_cells_bytes());
   L.per_image_base = al(L.bcnt + (size_t)n * kPrepB * kMaxNc * 4);
   size_t o = 0;
   // keys: a class at bucket offset `off` with S rows sorts at keys + 2*off; its
@@ -151,8 +164,11 @@ __host__ __device__ inline bool fast_task(int S);
 
 struct Hdr {
   int ntasks;  // the fast list: classes the LDS-resident path takes (nms_fast)
-  int nwide;   // the wide list (nms_wide / the r02 general path): the others
+  int nwide;   // the wide list (nms_wide_a's work in nms_fast, then nms_search / nms_resolve)
 };
+
+// Whether the fast classes of this batch are split (kSplitTasks); every kernel decides alike.
+__device__ __forceinline__ bool split_fast(const Hdr* h) { return h->ntasks + h->nwide <= kSplitTasks; }
 
 // Sort key within a class: score descending (inverted fp32 bits; scores are
 // products of sigmoids, never negative), then row ascending (stable sort).
@@ -906,6 +922,7 @@ __host__ __device__ inline int wide_min_s() {
 #endif
 }
 __host__ __device__ inline size_t wide_cells_bytes() { return ((size_t)kFCells * 4 + 255) & ~(size_t)255; }
+__host__ __device__ inline size_t fast_cells_bytes() { return (size_t)kFCellBytes; }  // u16 cell ends
 struct WFrame {
   float X0, Y0, inv;
   int img, cls, off, S, slot;
@@ -1019,7 +1036,7 @@ __device__ __forceinline__ void replace_slot16(unsigned short* sl, int rj) {
 template <int E>
 __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restrict__ ci, const Ptrs& P, char* smem, int (*s_lv)[5],
                          int* s_ext, int* s_w, int* s_flag, const Thr& thr, float t_lo, float inv_t, int all_pairs,
-                         unsigned long long* s_prof, unsigned long long* s_msk) {
+                         unsigned long long* s_prof, unsigned long long* s_msk, WFrame* pub, char* pub_cells) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int S = tk.S, off = tk.off;
   const int* bucket = P.bucket + off;
@@ -1178,6 +1195,22 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
   }
   __syncthreads();
   YCX_PROF_MARK(1)
+  if (pub) {  // split: the search and the fixed point run in nms_search / nms_resolve
+    unsigned* gc = reinterpret_cast<unsigned*>(pub_cells);
+    for (int k = tid; k < kFCellBytes / 4; k += kBigThreads) gc[k] = cells[k];
+    if (tid == 0) {
+      pub->X0 = X0;
+      pub->Y0 = Y0;
+      pub->inv = inv;
+      pub->img = tk.img;
+      pub->cls = tk.cls;
+      pub->off = off;
+      pub->S = S;
+    }
+    if (tid < kFLevels * 5) pub->lv[tid / 5][tid % 5] = s_lv[tid / 5][tid % 5];
+    __syncthreads();  // every read of the LDS done before the next task reuses it
+    return;
+  }
   // (4) suppressors of every box (spatial order), kSlots highest-ranked kept (global slots)
 #ifdef YCX_NMS_PROFILE
   const unsigned long long w_t0 = __builtin_amdgcn_s_memtime();
@@ -1358,7 +1391,7 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
 // ---------------------------------------------------------------------------
 // The LDS-resident classes (S <= kFastMax and fast_lds_bytes(S) fits): big_fast, one
 // 1024-thread workgroup per class (grid-strided task loop); nms_big then takes the rest.
-__device__ __attribute__((noinline)) void wide_a_task(const ycx_nms_desc& d, const ycx_cand* __restrict__ cand, char* ws,
+__device__ __forceinline__ void wide_a_task(const ycx_nms_desc& d, const ycx_cand* __restrict__ cand, char* ws,
                                             const Layout& L, int t, const Task& tk, char* smem, int (*s_lv)[5],
                                             int* s_ext, int* s_w, unsigned long long* s_msk, int all_pairs);
 
@@ -1406,7 +1439,10 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
       s_lv[tid][1] = s_lv[tid][2] = 0;  // +0.0f
       s_lv[tid][3] = s_lv[tid][4] = 0x7F800000;  // +inf
     }
-    big_fast<E>(tk, ci, P, smem, s_lv, s_ext, s_w, &s_flag, thr, t_lo, inv_t, all_pairs, s_prof, s_msk);
+    const bool split = with_wide && split_fast(hdr);
+    WFrame* pub = split ? reinterpret_cast<WFrame*>(ws + L.fframes + (size_t)t * wframe_bytes()) : nullptr;
+    char* pub_cells = ws + L.fcells + (size_t)t * fast_cells_bytes();
+    big_fast<E>(tk, ci, P, smem, s_lv, s_ext, s_w, &s_flag, thr, t_lo, inv_t, all_pairs, s_prof, s_msk, pub, pub_cells);
   }
 }
 
@@ -1440,14 +1476,16 @@ __device__ __forceinline__ void replace_slot32(int* sl, int rj) {  // keep the k
   if (rj < vm) sl[km] = rj;
 }
 
-// Stable LSD radix sort (4-bit digits, digits every key shares skipped) of S 64-bit keys
-// in global memory, ping-ponging between a and b; returns the buffer holding the result.
-// Striped layout (coalesced): element p = i * kBigThreads + tid, i < E = ceil(S / kBigThreads)
-// <= 128. A pass counts, per (digit, i, wave), the wave's elements of slot i with that digit
-// (the lanes with equal digits found by four ballots), scans the counts in (digit, i, wave)
-// order -- the input order within each digit -- and scatters every key to its count's
-// offset plus its rank among the equal-digit lanes below it: stable.
-// C = LDS u32 [16][E][16] (<= 128 KiB).
+// Stable LSD rank sort (4-bit digits, digits every key shares skipped) of a wide class's S
+// keys (score desc, row asc) in global scratch. Striped layout (coalesced): element p = i *
+// kBigThreads + tid, i < E = ceil(S / kBigThreads) <= 128. A pass counts, per (digit, i, wave),
+// the wave's elements of slot i with that digit (the lanes with equal digits found by four
+// ballots), scans the counts in (digit, i, wave) order -- the input order within each digit --
+// and scatters every key to its count's offset plus its rank among the equal-digit lanes below
+// it: stable, and the lanes of a group write consecutive addresses. Keys move in batches of 8
+// slots per thread with the batch's loads issued together (one memory round trip per 8 keys,
+// not per key); the last pass scatters the rows themselves into bucket (rank order).
+// a / b: 8 S bytes each; C: LDS u32 [16][E][16] (<= 128 KiB).
 __device__ __forceinline__ unsigned long long same_digit_lanes(int dg) {
   unsigned long long m = ~0ull;
 #pragma unroll
@@ -1458,19 +1496,27 @@ __device__ __forceinline__ unsigned long long same_digit_lanes(int dg) {
   return m;
 }
 
-__device__ unsigned long long* radix_sort_global(unsigned long long* a, unsigned long long* b, int S,
-                                                 unsigned* C, int* s_w, unsigned long long* s_msk) {
+__device__ void radix_rank(const ycx_cand* __restrict__ ci, int* bucket, int S, unsigned long long* a,
+                           unsigned long long* b, unsigned* C, int* s_w, unsigned long long* s_msk) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int NW = kBigThreads / 64;
   const int E = (S + kBigThreads - 1) / kBigThreads;
+  const int nch = (E + 7) / 8;  // uniform
   const unsigned long long lt = (1ull << lane) - 1ull;  // lanes below this one
+  auto at = [&](int c, int j) { return (8 * c + j) * kBigThreads + tid; };
   unsigned long long an = ~0ull, orr = 0ull;
-  for (int i = 0; i < E; ++i) {
-    const int p = i * kBigThreads + tid;
-    if (p < S) {
-      const unsigned long long k = a[p];
-      an &= k;
-      orr |= k;
+  for (int c = 0; c < nch; ++c) {  // keys built from the candidates into a
+    int row[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) row[j] = at(c, j) < S ? bucket[at(c, j)] : -1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (row[j] >= 0) {
+        const unsigned long long key = make_key(ci[row[j]]);
+        a[at(c, j)] = key;
+        an &= key;
+        orr |= key;
+      }
     }
   }
 #pragma unroll
@@ -1479,24 +1525,34 @@ __device__ unsigned long long* radix_sort_global(unsigned long long* a, unsigned
     orr |= __shfl_xor(orr, sh);
   }
   if (tid == 0) { s_msk[0] = ~0ull; s_msk[1] = 0ull; }
-  __syncthreads();
+  __syncthreads();  // every bucket read done (the last pass rewrites bucket)
   if (lane == 0) {
     atomicAnd(&s_msk[0], an);
     atomicOr(&s_msk[1], orr);
   }
   __syncthreads();
   const unsigned long long diff = s_msk[0] ^ s_msk[1];
+  int last = -1;  // the last digit any two keys differ in (none: S == 1, bucket already in order)
+  for (int sh = 0; sh < 64; sh += 4)
+    if ((diff >> sh) & 0xF) last = sh;
   const int nC = 16 * E * NW;
-  for (int sh = 0; sh < 64; sh += 4) {
+  for (int sh = 0; sh <= last; sh += 4) {
     if (((diff >> sh) & 0xF) == 0) continue;  // uniform
     for (int c = tid; c < nC; c += kBigThreads) C[c] = 0;
     __syncthreads();
-    for (int i = 0; i < E; ++i) {  // uniform trip count: the ballots need every lane
-      const int p = i * kBigThreads + tid;
-      const bool ok = p < S;
-      const int dg = ok ? (int)((a[p] >> sh) & 0xF) : 16;  // 16: past the end (matches no digit)
-      const unsigned long long m = same_digit_lanes(dg & 15) & __ballot(ok);
-      if (ok && (m & lt) == 0) C[(dg * E + i) * NW + wid] = (unsigned)__popcll(m);  // the group's first lane
+    for (int c = 0; c < nch; ++c) {
+      unsigned long long k[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) k[j] = at(c, j) < S ? a[at(c, j)] : 0ull;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * c + j;
+        if (i >= E) break;  // uniform: the ballots need every lane
+        const bool ok = at(c, j) < S;
+        const int dg = ok ? (int)((k[j] >> sh) & 0xF) : 16;  // 16: past the end (matches no digit)
+        const unsigned long long m = same_digit_lanes(dg & 15) & __ballot(ok);
+        if (ok && (m & lt) == 0) C[(dg * E + i) * NW + wid] = (unsigned)__popcll(m);  // the group's first lane
+      }
     }
     __syncthreads();
     {  // exclusive scan of C in (digit, i, wave) order: thread t owns a contiguous run
@@ -1512,26 +1568,36 @@ __device__ unsigned long long* radix_sort_global(unsigned long long* a, unsigned
       }
     }
     __syncthreads();
-    for (int i = 0; i < E; ++i) {
-      const int p = i * kBigThreads + tid;
-      const bool ok = p < S;
-      const unsigned long long k = ok ? a[p] : 0ull;
-      const int dg = ok ? (int)((k >> sh) & 0xF) : 16;
-      const unsigned long long m = same_digit_lanes(dg & 15) & __ballot(ok);
-      if (ok) b[C[(dg * E + i) * NW + wid] + __popcll(m & lt)] = k;
+    const bool fin = sh == last;
+    for (int c = 0; c < nch; ++c) {
+      unsigned long long k[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) k[j] = at(c, j) < S ? a[at(c, j)] : 0ull;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * c + j;
+        if (i >= E) break;
+        const bool ok = at(c, j) < S;
+        const int dg = ok ? (int)((k[j] >> sh) & 0xF) : 16;
+        const unsigned long long m = same_digit_lanes(dg & 15) & __ballot(ok);
+        if (ok) {
+          const unsigned q = C[(dg * E + i) * NW + wid] + (unsigned)__popcll(m & lt);
+          if (fin) bucket[q] = (int)(unsigned)k[j];
+          else b[q] = k[j];
+        }
+      }
     }
-    __syncthreads();  // b complete (and every read of a and C done) before the next pass
+    __syncthreads();  // the pass's output complete (and every read of a and C done) before the next pass
     unsigned long long* t = a;
     a = b;
     b = t;
   }
-  return a;
 }
 
 // nms_wide_a's work for wide task t: the class's keys sorted, boxes in rank order, the
 // spatial index published for nms_wide_s / nms_wide_b (run inside nms_fast's launch, beside
 // the fast classes: both are one workgroup per class and neither waits on the other)
-__device__ __attribute__((noinline)) void wide_a_task(const ycx_nms_desc& d, const ycx_cand* __restrict__ cand, char* ws,
+__device__ __forceinline__ void wide_a_task(const ycx_nms_desc& d, const ycx_cand* __restrict__ cand, char* ws,
                                             const Layout& L, int t, const Task& tk, char* smem, int (*s_lv)[5],
                                             int* s_ext, int* s_w, unsigned long long* s_msk, int all_pairs) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1554,34 +1620,38 @@ __device__ __attribute__((noinline)) void wide_a_task(const ycx_nms_desc& d, con
       s_lv[tid][1] = s_lv[tid][2] = 0;
       s_lv[tid][3] = s_lv[tid][4] = 0x7F800000;
     }
-    // (1) keys (score desc, row asc) in the workspace, radix-sorted: rank r = position
+    // (1) keys (score desc, row asc), radix-sorted: rank r = position; bucket in rank order
     unsigned long long* ka = P.keys + 2 * (size_t)off;
-    for (int e0 = tid; e0 < S; e0 += 4 * kBigThreads) {  // four gathers in flight per thread
-      int row[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) row[u] = e0 + u * kBigThreads < S ? bucket[e0 + u * kBigThreads] : -1;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (row[u] >= 0) ka[e0 + u * kBigThreads] = make_key(ci[row[u]]);
-    }
-    __syncthreads();
-    const unsigned long long* sorted =
-        radix_sort_global(ka, ka + S, S, reinterpret_cast<unsigned*>(smem), s_w, s_msk);
-    for (int r = tid; r < S; r += kBigThreads) bucket[r] = (int)(unsigned)sorted[r];  // bucket in rank order
+    radix_rank(ci, bucket, S, ka, ka + S, reinterpret_cast<unsigned*>(smem), s_w, s_msk);
     __syncthreads();
     YCX_WPROF_MARK(0)
     // (2) boxes in rank order (the dead keys' region, 16 B per rank) and the class extent
     f32x4* rbox = reinterpret_cast<f32x4*>(ka);
     {
       int mn0 = 0x7FFFFFFF, mn1 = 0x7FFFFFFF, mx2 = (int)0x80000000, mx3 = (int)0x80000000;
-      for (int r = tid; r < S; r += kBigThreads) {
-        const ycx_cand c = ci[bucket[r]];  // (the loop body is small: the compiler keeps several in flight)
-        rbox[r] = f32x4{c.x1, c.y1, c.x2, c.y2};
-        if (c.x2 > c.x1 && c.y2 > c.y1 && c.x1 > -INFINITY && c.y1 > -INFINITY && c.x2 < INFINITY && c.y2 < INFINITY) {
-          mn0 = min(mn0, f2o(c.x1));
-          mn1 = min(mn1, f2o(c.y1));
-          mx2 = max(mx2, f2o(c.x2));
-          mx3 = max(mx3, f2o(c.y2));
+      for (int r0 = tid; r0 < S; r0 += 8 * kBigThreads) {  // batches of 8 ranks: the loads issued together
+        int row[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) row[j] = r0 + j * kBigThreads < S ? bucket[r0 + j * kBigThreads] : -1;
+        f32x4 bx[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (row[j] >= 0) {
+            const ycx_cand& c = ci[row[j]];
+            bx[j] = f32x4{c.x1, c.y1, c.x2, c.y2};
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (row[j] < 0) continue;
+          const f32x4 c = bx[j];
+          rbox[r0 + j * kBigThreads] = c;
+          if (c[2] > c[0] && c[3] > c[1] && c[0] > -INFINITY && c[1] > -INFINITY && c[2] < INFINITY && c[3] < INFINITY) {
+            mn0 = min(mn0, f2o(c[0]));
+            mn1 = min(mn1, f2o(c[1]));
+            mx2 = max(mx2, f2o(c[2]));
+            mx3 = max(mx3, f2o(c[3]));
+          }
         }
       }
 #pragma unroll
@@ -1604,12 +1674,21 @@ __device__ __attribute__((noinline)) void wide_a_task(const ycx_nms_desc& d, con
     const float Ex = fmaxf(o2f(s_ext[2]) - X0, o2f(s_ext[3]) - Y0);
     const float inv = (Ex > 0.0f && Ex < INFINITY) ? 1.0f / Ex : 0.0f;
     // (3) spatial counting sort on the fine grid (uniform trip count: the level ballots)
-    for (int r0 = 0; r0 < S; r0 += kBigThreads) {
-      const int r = r0 + tid;
+    for (int rb = 0; rb < S; rb += 8 * kBigThreads) {  // batches of 8 ranks per thread
+      f32x4 bx[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = rb + j * kBigThreads + tid;
+        if (r < S) bx[j] = rbox[r];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+      const int r = rb + j * kBigThreads + tid;
+      if (rb + j * kBigThreads >= S) break;  // uniform: the level ballots need every lane
       FGeo g;
       g.level = -1;
       if (r < S) {
-        g = fgeometry(rbox[r], X0, Y0, inv, all_pairs);
+        g = fgeometry(bx[j], X0, Y0, inv, all_pairs);
         atomicAdd(&cells[g.cell], 1u);
       }
       for (int Lv = 0; Lv < kFLevels; ++Lv) {
@@ -1633,6 +1712,7 @@ __device__ __attribute__((noinline)) void wide_a_task(const ycx_nms_desc& d, con
           atomicMin(&s_lv[Lv][4], mnh);
         }
       }
+      }
     }
     __syncthreads();
     {  // exclusive scan of the cell counts in place
@@ -1652,11 +1732,19 @@ __device__ __attribute__((noinline)) void wide_a_task(const ycx_nms_desc& d, con
     __syncthreads();
     f32x4* sbox = P.sbox + off;
     int* srank = P.srank + off;
-    for (int r = tid; r < S; r += kBigThreads) {
-      const f32x4 b = rbox[r];
-      const int q = (int)atomicAdd(&cells[fgeometry(b, X0, Y0, inv, all_pairs).cell], 1u);  // -> cell ends
-      sbox[q] = b;
-      srank[q] = r;
+    for (int r0 = tid; r0 < S; r0 += 8 * kBigThreads) {  // batches of 8 ranks per thread
+      f32x4 bx[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (r0 + j * kBigThreads < S) bx[j] = rbox[r0 + j * kBigThreads];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = r0 + j * kBigThreads;
+        if (r >= S) continue;
+        const int q = (int)atomicAdd(&cells[fgeometry(bx[j], X0, Y0, inv, all_pairs).cell], 1u);  // -> cell ends
+        sbox[q] = bx[j];
+        srank[q] = r;
+      }
     }
     __syncthreads();
     // publish the class's spatial index for the search and resolve launches
@@ -1677,8 +1765,6 @@ __device__ __attribute__((noinline)) void wide_a_task(const ycx_nms_desc& d, con
     __syncthreads();
 }
 
-constexpr int kWChunk = 2048;  // positions per nms_wide_s item
-
 // load a wide class's frame (level stats to LDS) and cell table (to LDS); returns the frame
 __device__ __forceinline__ WFrame load_wide(const char* ws, const Layout& L, int t, unsigned* cells, int (*s_lv)[5]) {
   const WFrame* fr = reinterpret_cast<const WFrame*>(ws + L.wframes + (size_t)t * wframe_bytes());
@@ -1690,159 +1776,412 @@ __device__ __forceinline__ WFrame load_wide(const char* ws, const Layout& L, int
   return f;
 }
 
-// Suppressor search of the wide classes, split into items of kWChunk positions so a
-// class's search runs on many CUs (one workgroup per item, grid-strided).
-__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_wide_s(
-    ycx_nms_desc d, char* ws, Thr thr, float t_lo, float inv_t, int all_pairs) {
-  __shared__ __attribute__((aligned(16))) unsigned cells[kFCells];
-  __shared__ int s_lv[kFLevels][5];
-  const int tid = threadIdx.x;
-  const Layout L = layout(d.n, d.rows_total);
-  const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
-  const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks) + (size_t)d.n * L.max_tasks;
-  const int ntasks = hdr->nwide;
-  int nitems = 0;
-  for (int t = 0; t < ntasks; ++t) nitems += (tasks[t].S + kWChunk - 1) / kWChunk;
-  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
-    int t = 0, c = item;  // the item's class and chunk (uniform scan of the short task list)
-    while (c >= (tasks[t].S + kWChunk - 1) / kWChunk) {
-      c -= (tasks[t].S + kWChunk - 1) / kWChunk;
-      ++t;
-    }
-    const WFrame f = load_wide(ws, L, t, cells, s_lv);
-    const Ptrs P = image_ptrs(ws, L, f.img);
-    const int S = f.S, off = f.off;
-    const f32x4* sbox = P.sbox + off;
-    const int* srank = P.srank + off;
-    auto cend = [&](int k) { return (int)cells[k]; };
-    const int p1 = min(S, (c + 1) * kWChunk);
-    for (int p = c * kWChunk + tid; p < p1; p += kBigThreads) {
-      const int r = srank[p];
-      const f32x4 b = sbox[p];
-      const float a = box_area(b);
-      const FGeo g = fgeometry(b, f.X0, f.Y0, f.inv, all_pairs);
-      int* sl = P.slots + (size_t)(off + p) * kSlots;
-      int ns = 0;
-      auto test = [&](int rj, const f32x4& o) {
-        const bool cnd = rj < r && (all_pairs || (o[0] < b[2] && o[2] > b[0] && o[1] < b[3] && o[3] > b[1]));
-        if (cnd && suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
+// the same for a split fast class (u16 cell ends, copied as packed words)
+__device__ __forceinline__ WFrame load_fast(const char* ws, const Layout& L, int t, unsigned* cells, int (*s_lv)[5]) {
+  const WFrame* fr = reinterpret_cast<const WFrame*>(ws + L.fframes + (size_t)t * wframe_bytes());
+  const unsigned* gcells = reinterpret_cast<const unsigned*>(ws + L.fcells + (size_t)t * fast_cells_bytes());
+  for (int k = threadIdx.x; k < kFCellBytes / 4; k += kBigThreads) cells[k] = gcells[k];
+  if (threadIdx.x < kFLevels * 5) s_lv[threadIdx.x / 5][threadIdx.x % 5] = fr->lv[threadIdx.x / 5][threadIdx.x % 5];
+  const WFrame f = *fr;
+  __syncthreads();
+  return f;
+}
+
+// The classes nms_search and nms_resolve take: the wide list, then (split) the fast list.
+struct BigList {
+  const Task* wide;
+  const Task* fast;
+  int nwide, nfast;
+  __device__ __forceinline__ int size() const { return nwide + nfast; }
+  __device__ __forceinline__ int S(int t) const { return t < nwide ? wide[t].S : fast[t - nwide].S; }
+};
+
+__device__ __forceinline__ BigList big_list(const char* ws, const Layout& L, int n) {
+  const Hdr* h = reinterpret_cast<const Hdr*>(ws + L.hdr);
+  const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks);
+  BigList b;
+  b.wide = tasks + (size_t)n * L.max_tasks;
+  b.fast = tasks;
+  b.nwide = h->nwide;
+  b.nfast = split_fast(h) ? h->ntasks : 0;
+  return b;
+}
+
+// Suppressor search of positions [p0, p1) of one class (spatial order): every box's
+// higher-ranked boxes with IoU > thr, the highest-ranked kept in its 64-byte slot row
+// (kFast: 32 u16 ranks, the fast path's format; else 16 int ranks) and their count.
+template <bool kFast, class RankT>
+__device__ __forceinline__ void search_range(const WFrame& f, const unsigned* cells, const int (*s_lv)[5],
+                                             const f32x4* sbox, const RankT* srank, const Ptrs& P, int p0,
+                                             int p1, const Thr& thr, float t_lo, float inv_t, int all_pairs) {
+  const int S = f.S, off = f.off;
+  auto cend = [&](int k) -> int {
+    if constexpr (kFast) return u16_at(cells, k);
+    else return (int)cells[k];
+  };
+  for (int p = p0 + (int)threadIdx.x; p < p1; p += kBigThreads) {
+    const int r = (int)srank[p];
+    const f32x4 b = sbox[p];
+    const float a = box_area(b);
+    const FGeo g = fgeometry(b, f.X0, f.Y0, f.inv, all_pairs);
+    int* sl = P.slots + (size_t)(off + p) * kSlots;
+    int ns = 0;
+    auto test = [&](int rj, const f32x4& o) {
+      const bool cnd = rj < r && (all_pairs || (o[0] < b[2] && o[2] > b[0] && o[1] < b[3] && o[3] > b[1]));
+      if (cnd && suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
+        if constexpr (kFast) {
+          unsigned short* s16 = reinterpret_cast<unsigned short*>(sl);
+          if (ns < kFSlots) s16[ns] = (unsigned short)rj;
+          else replace_slot16(s16, rj);
+        } else {
           if (ns < kSlots) sl[ns] = rj;
           else replace_slot32(sl, rj);
-          ++ns;
         }
-      };
-      f_ranges(cend, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
-        int q = q0;
-        for (; q + 4 <= q1; q += 4) {
-          int rj[4];
-          f32x4 o[4];
+        ++ns;
+      }
+    };
+    f_ranges(cend, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
+      int q = q0;
+      for (; q + 4 <= q1; q += 4) {
+        int rj[4];
+        f32x4 o[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            rj[u] = srank[q + u];
-            o[u] = sbox[q + u];
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) test(rj[u], o[u]);
+        for (int u = 0; u < 4; ++u) {
+          rj[u] = (int)srank[q + u];
+          o[u] = sbox[q + u];
         }
-        for (; q < q1; ++q) test(srank[q], sbox[q]);
-      });
-      P.nsup[off + p] = ns;
-    }
-    __syncthreads();  // every read of this item's cells done before the next item loads its own
+#pragma unroll
+        for (int u = 0; u < 4; ++u) test(rj[u], o[u]);
+      }
+      for (; q < q1; ++q) test((int)srank[q], sbox[q]);
+    });
+    P.nsup[off + p] = ns;
   }
 }
 
-// Greedy fixed point and compaction of the wide classes (one workgroup per class).
-__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_wide_b(
+// Suppressor search of every split class: the concatenated positions of the list are cut into
+// gridDim.x equal ranges, one per workgroup (a range may span classes: each class's index is
+// staged in LDS once per workgroup), so the whole grid shares the search however few and
+// however unequal the classes are.
+__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_search(
     ycx_nms_desc d, char* ws, Thr thr, float t_lo, float inv_t, int all_pairs) {
+  // a wide class: its u32 cell ends; a fast class: u16 cell ends, then its boxes and u16 ranks
+  // in spatial order (what its own search read from LDS in nms_fast): fast_lds_bytes(S) fits
+  __shared__ __attribute__((aligned(16))) char smem[kBigLds];
+  __shared__ int s_lv[kFLevels][5];
+  unsigned* cells = reinterpret_cast<unsigned*>(smem);
+  const Layout L = layout(d.n, d.rows_total);
+  const BigList bl = big_list(ws, L, d.n);
+  const int nt = bl.size();
+  long long tot = 0;
+  for (int t = 0; t < nt; ++t) tot += bl.S(t);
+  const long long lo = tot * blockIdx.x / gridDim.x, hi = tot * (blockIdx.x + 1) / gridDim.x;
+  long long s0 = 0;
+  for (int t = 0; t < nt && s0 < hi; ++t) {  // bounded: the list is finite
+    const int S = bl.S(t);
+    const long long a = lo > s0 ? lo : s0, b = hi < s0 + S ? hi : s0 + S;
+    if (a < b) {
+      if (t >= bl.nwide) {
+        const WFrame f = load_fast(ws, L, t - bl.nwide, cells, s_lv);
+        const Ptrs P = image_ptrs(ws, L, f.img);
+        f32x4* lbox = reinterpret_cast<f32x4*>(smem + kFCellBytes);
+        unsigned short* lr = reinterpret_cast<unsigned short*>(smem + kFCellBytes + 16 * S);
+        for (int p = threadIdx.x; p < S; p += kBigThreads) {
+          lbox[p] = P.sbox[f.off + p];
+          lr[p] = (unsigned short)P.srank[f.off + p];
+        }
+        __syncthreads();
+        search_range<true>(f, cells, s_lv, lbox, lr, P, (int)(a - s0), (int)(b - s0), thr, t_lo, inv_t, all_pairs);
+      } else {
+        const WFrame f = load_wide(ws, L, t, cells, s_lv);
+        const Ptrs P = image_ptrs(ws, L, f.img);
+        search_range<false>(f, cells, s_lv, P.sbox + f.off, P.srank + f.off, P, (int)(a - s0), (int)(b - s0), thr,
+                            t_lo, inv_t, all_pairs);
+      }
+      __syncthreads();  // every read of this class's LDS done before the next one is staged
+    }
+    s0 += S;
+  }
+}
+
+// Greedy fixed point of a wide class (one workgroup): positions p = tid + k * kBigThreads,
+// k < E; each thread tracks its undecided positions in a bit mask (only the owner of a position
+// ever decides its rank), so a round touches only those, two at a time with their rank, count
+// and 64-byte slot row loaded together. Then the kept rows in rank order (each thread a
+// contiguous run of ranks, one scan).
+__device__ __forceinline__ void resolve_wide(const Layout& L, char* ws, int t, const Task tk, char* smem,
+                                                       int (*s_lv)[5], int* s_w, int* s_flag, const Thr thr,
+                                                       float t_lo, float inv_t, int all_pairs) {
   constexpr int kCellB = ((kFCells * 4) + 255) & ~255;  // u32 cell ends
+  const int tid = threadIdx.x;
+  unsigned* cells = reinterpret_cast<unsigned*>(smem);
+#ifdef YCX_NMS_PROFILE
+  unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
+#endif
+  const WFrame f = load_wide(ws, L, t, cells, s_lv);
+  const Ptrs P = image_ptrs(ws, L, tk.img);
+  const int S = tk.S, off = tk.off;
+  const int* bucket = P.bucket + off;
+  const f32x4* sbox = P.sbox + off;
+  const int* srank = P.srank + off;
+  const int* nsup = P.nsup + off;
+  const int4* slots = reinterpret_cast<const int4*>(P.slots + (size_t)off * kSlots);
+  auto cend = [&](int k) { return (int)cells[k]; };
+  unsigned char* st = S <= kBigLds - kCellB ? reinterpret_cast<unsigned char*>(smem + kCellB) : P.state + off;
+  for (int r = tid; r < S; r += kBigThreads) st[r] = 0;
+  const int E = (S + kBigThreads - 1) / kBigThreads;  // <= kMaxRows / kBigThreads = 128
+  unsigned und[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int kn = min(32, max(0, E - 32 * w));  // slots k of this word below E
+    unsigned m = kn == 32 ? ~0u : ((1u << kn) - 1u);
+    if (kn > 0 && tid + (32 * w + kn - 1) * kBigThreads >= S) m &= ~(1u << (kn - 1));  // the last slot may be past S
+    und[w] = m;
+  }
+  __syncthreads();
+  YCX_WPROF_MARK(2)
+  // res: 0 every suppressor removed (keep), 1 some undecided, 2 one kept (remove)
+  auto decide = [&](int p, int r, int ns, const int4 (&s)[4]) -> int {
+    int res = 0;
+    const int c = min(ns, kSlots);
+#pragma unroll
+    for (int h = 0; h < kSlots; ++h) {
+      const int4 x = s[h >> 2];
+      const int v = (h & 3) == 0 ? x.x : (h & 3) == 1 ? x.y : (h & 3) == 2 ? x.z : x.w;
+      if (h < c && res != 2) {
+        const unsigned char sj = st[v];
+        res = sj == 1 ? 2 : (sj == 0 ? 1 : res);
+      }
+    }
+    if (ns > kSlots && res == 0) {  // the cached ones are all removed: rescan
+      const f32x4 b = sbox[p];
+      const float a = box_area(b);
+      const FGeo g = fgeometry(b, f.X0, f.Y0, f.inv, all_pairs);
+      bool stop = false;
+      f_ranges(cend, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
+        for (int q = q0; q < q1 && !stop; ++q) {
+          const int rj = srank[q];
+          if (rj >= r) continue;
+          const unsigned char sj = st[rj];
+          if (sj == 2) continue;
+          const f32x4 o = sbox[q];
+          if (suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
+            if (sj == 1) { res = 2; stop = true; }
+            else res = 1;
+          }
+        }
+      });
+    }
+    return res;
+  };
+  for (int it = 0; it <= S; ++it) {  // every round decides at least one box
+    if (tid == 0) *s_flag = 0;
+    __syncthreads();
+    int undecided = 0;
+#ifdef YCX_NMS_PROFILE
+    unsigned und0[4] = {und[0], und[1], und[2], und[3]};
+#endif
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      unsigned m = und[w];
+      while (m) {
+        const int k0 = 32 * w + __builtin_ctz(m);
+        m &= m - 1u;
+        const int k1 = m ? 32 * w + __builtin_ctz(m) : -1;
+        if (m) m &= m - 1u;
+        const int pa = tid + k0 * kBigThreads, pb = k1 >= 0 ? tid + k1 * kBigThreads : pa;
+        const int ra = srank[pa], rb = srank[pb];
+        const int na = nsup[pa], nb = nsup[pb];
+        int4 sa[4], sb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sa[q] = slots[(size_t)pa * 4 + q];
+          sb[q] = slots[(size_t)pb * 4 + q];
+        }
+        const int resa = decide(pa, ra, na, sa);
+        if (resa == 1) {
+          undecided = 1;
+        } else {
+          st[ra] = resa == 2 ? 2 : 1;
+          und[w] &= ~(1u << (k0 & 31));
+        }
+        if (k1 >= 0) {
+          const int resb = decide(pb, rb, nb, sb);
+          if (resb == 1) {
+            undecided = 1;
+          } else {
+            st[rb] = resb == 2 ? 2 : 1;
+            und[w] &= ~(1u << (k1 & 31));
+          }
+        }
+      }
+    }
+    if (undecided) *s_flag = 1;
+#ifdef YCX_NMS_PROFILE
+    {  // positions this round looked at (undecided at its start), summed over the waves
+      int v = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) v += __popc(und0[w]);
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if ((tid & 63) == 0) atomicAdd(&g_nms_wprof[6], (unsigned long long)v);
+    }
+#endif
+    __syncthreads();
+    const int more = *s_flag;
+    __syncthreads();
+#ifdef YCX_NMS_PROFILE
+    if (tid == 0) atomicAdd(&g_nms_wprof[5], 1ull);
+#endif
+    if (!more) break;
+  }
+  YCX_WPROF_MARK(3)
+  const int r0 = min(S, tid * E), r1 = min(S, r0 + E);
+  int nk = 0;
+  for (int r = r0; r < r1; ++r) nk += st[r] == 1 ? 1 : 0;
+  int kt;
+  int pos = block_exclusive(nk, s_w, &kt);
+  for (int r = r0; r < r1; ++r)
+    if (st[r] == 1) P.kept[off + pos++] = bucket[r];
+  if (tid == 0) P.kc[tk.cls] = kt;
+  __syncthreads();
+  YCX_WPROF_MARK(4)
+}
+
+// Greedy fixed point of a split fast class (one workgroup): the fast path's phases (5)-(7)
+// with the ranks by position (u16) and the suppressor lists (CSR) staged in LDS from the
+// search's global output, undecided positions tracked per thread as in resolve_wide.
+__device__ __forceinline__ void resolve_fast(const Layout& L, char* ws, int t, char* smem,
+                                                       int (*s_lv)[5], int* s_w, int* s_flag, const Thr thr,
+                                                       float t_lo, float inv_t, int all_pairs) {
+  const int tid = threadIdx.x;
+  const WFrame* fr = reinterpret_cast<const WFrame*>(ws + L.fframes + (size_t)t * wframe_bytes());
+  const unsigned* gcells = reinterpret_cast<const unsigned*>(ws + L.fcells + (size_t)t * fast_cells_bytes());
+  if (tid < kFLevels * 5) s_lv[tid / 5][tid % 5] = fr->lv[tid / 5][tid % 5];
+  const WFrame f = *fr;
+  const Ptrs P = image_ptrs(ws, L, f.img);
+  const int S = f.S, off = f.off;
+  const f32x4* sbox = P.sbox + off;
+  const int* srank = P.srank + off;
+  const int* nsup = P.nsup + off;
+  const unsigned short* gsl = reinterpret_cast<const unsigned short*>(P.slots + (size_t)off * kSlots);
+  unsigned short* lr = reinterpret_cast<unsigned short*>(smem);                              // [S]
+  unsigned char* st = reinterpret_cast<unsigned char*>(smem + ((2 * S + 15) & ~15));          // [S]
+  unsigned* csr_off = reinterpret_cast<unsigned*>(smem + ((2 * S + 15) & ~15) + ((S + 15) & ~15));  // [S]
+  unsigned short* csr_ns = reinterpret_cast<unsigned short*>(csr_off + S);                    // [S]
+  unsigned short* csr = csr_ns + ((S + 1) & ~1);                                              // [total]
+  const int E = (S + kBigThreads - 1) / kBigThreads;  // <= kFastMax / kBigThreads = 8
+  int my_total = 0;
+  for (int k = 0; k < E; ++k) {
+    const int p = tid + k * kBigThreads;
+    if (p < S) {
+      lr[p] = (unsigned short)srank[p];
+      st[p] = 0;
+      my_total += min(nsup[p], kFSlots);
+    }
+  }
+  int total;
+  int base = block_exclusive(my_total, s_w, &total);
+  const size_t csr_end = (size_t)(((2 * S + 15) & ~15) + ((S + 15) & ~15)) + 4 * (size_t)S + 2 * (size_t)((S + 1) & ~1) +
+                         2 * (size_t)total;
+  const bool lds_csr = csr_end <= (size_t)kBigLds;
+  if (lds_csr) {
+    for (int k = 0; k < E; ++k) {
+      const int p = tid + k * kBigThreads;
+      if (p >= S) break;
+      const int ns = nsup[p], c = min(ns, kFSlots);
+      for_slots16(gsl + (size_t)p * (2 * kSlots), c, [&](int j, int v) { csr[base + j] = (unsigned short)v; });
+      csr_off[p] = base;
+      csr_ns[p] = (unsigned short)min(ns, 0xFFFF);
+      base += c;
+    }
+  }
+  unsigned und = 0;
+  for (int k = 0; k < E; ++k)
+    if (tid + k * kBigThreads < S) und |= 1u << k;
+  __syncthreads();
+  auto cend = [&](int k) { return u16_at(gcells, k); };
+  for (int it = 0; it <= S; ++it) {  // every round decides at least one box
+    if (tid == 0) *s_flag = 0;
+    __syncthreads();
+    int undecided = 0;
+    unsigned m = und;
+    while (m) {
+      const int k = __builtin_ctz(m);
+      m &= m - 1u;
+      const int p = tid + k * kBigThreads;
+      const int r = lr[p];
+      int ns, res = 0;
+      if (lds_csr) {
+        ns = csr_ns[p];
+        const int b0 = csr_off[p], c = min(ns, kFSlots);
+        for (int j = 0; j < c && res != 2; ++j) {
+          const unsigned char sj = st[csr[b0 + j]];
+          res = sj == 1 ? 2 : (sj == 0 ? 1 : res);
+        }
+      } else {
+        ns = nsup[p];
+        for_slots16(gsl + (size_t)p * (2 * kSlots), min(ns, kFSlots), [&](int, int v) {
+          const unsigned char sj = st[v];
+          res = res == 2 ? 2 : (sj == 1 ? 2 : (sj == 0 ? 1 : res));
+        });
+      }
+      if (ns > kFSlots && res == 0) {  // the cached ones are all removed: rescan (global copies)
+        const f32x4 b = sbox[p];
+        const float a = box_area(b);
+        const FGeo g = fgeometry(b, f.X0, f.Y0, f.inv, all_pairs);
+        bool stop = false;
+        f_ranges(cend, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
+          for (int q = q0; q < q1 && !stop; ++q) {
+            const int rj = srank[q];
+            if (rj >= r) continue;
+            const unsigned char sj = st[rj];
+            if (sj == 2) continue;
+            const f32x4 o = sbox[q];
+            if (suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
+              if (sj == 1) { res = 2; stop = true; }
+              else res = 1;
+            }
+          }
+        });
+      }
+      if (res == 1) {
+        undecided = 1;
+      } else {
+        st[r] = res == 2 ? 2 : 1;
+        und &= ~(1u << k);
+      }
+    }
+    if (undecided) *s_flag = 1;
+    __syncthreads();
+    const int more = *s_flag;
+    __syncthreads();
+    if (!more) break;
+  }
+  const int r0 = min(S, tid * E), r1 = min(S, r0 + E);
+  int nk = 0;
+  for (int r = r0; r < r1; ++r) nk += st[r] == 1 ? 1 : 0;
+  int kt;
+  int pos = block_exclusive(nk, s_w, &kt);
+  const int* rank_row = P.bucket + off;
+  for (int r = r0; r < r1; ++r)
+    if (st[r] == 1) P.kept[off + pos++] = rank_row[r];
+  if (tid == 0) P.kc[f.cls] = kt;
+  __syncthreads();
+}
+
+// Fixed point and compaction of every split class, one workgroup per class (wide classes
+// first: the longest items).
+__global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_eu(4))) nms_resolve(
+    ycx_nms_desc d, char* ws, Thr thr, float t_lo, float inv_t, int all_pairs) {
   __shared__ __attribute__((aligned(16))) char smem[kBigLds];
   __shared__ int s_lv[kFLevels][5];
   __shared__ int s_w[kBigThreads / 64];
   __shared__ int s_flag;
-  const int tid = threadIdx.x;
   const Layout L = layout(d.n, d.rows_total);
-  const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
-  const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks) + (size_t)d.n * L.max_tasks;
-  const int ntasks = hdr->nwide;
-  unsigned* cells = reinterpret_cast<unsigned*>(smem);
-  for (int t = blockIdx.x; t < ntasks; t += gridDim.x) {
-    const Task tk = tasks[t];
-#ifdef YCX_NMS_PROFILE
-    unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
-#endif
-    const WFrame f = load_wide(ws, L, t, cells, s_lv);
-    const Ptrs P = image_ptrs(ws, L, tk.img);
-    const int S = tk.S, off = tk.off;
-    const int* bucket = P.bucket + off;
-    const float X0 = f.X0, Y0 = f.Y0, inv = f.inv;
-    const f32x4* sbox = P.sbox + off;
-    const int* srank = P.srank + off;
-    auto cend = [&](int k) { return (int)cells[k]; };
-    // (5) fixed point: state by rank in LDS beside the cells when it fits
-    unsigned char* st = S <= kBigLds - kCellB ? reinterpret_cast<unsigned char*>(smem + kCellB) : P.state + off;
-    for (int r = tid; r < S; r += kBigThreads) st[r] = 0;
-    __syncthreads();
-    YCX_WPROF_MARK(2)
-    for (int it = 0; it <= S; ++it) {  // every round decides at least one box
-      if (tid == 0) s_flag = 0;
-      __syncthreads();
-      int undecided = 0;
-      for (int p = tid; p < S; p += kBigThreads) {
-        const int r = srank[p];
-        if (st[r] != 0) continue;
-        const int ns = P.nsup[off + p];
-        int res = 0;  // 0: every suppressor removed, 1: some undecided, 2: one kept
-        for_slots32(P.slots + (size_t)(off + p) * kSlots, min(ns, kSlots), [&](int, int v) {
-          const unsigned char sj = st[v];
-          res = res == 2 ? 2 : (sj == 1 ? 2 : (sj == 0 ? 1 : res));
-        });
-        if (ns > kSlots && res == 0) {  // the cached ones are all removed: rescan
-          const f32x4 b = sbox[p];
-          const float a = box_area(b);
-          const FGeo g = fgeometry(b, X0, Y0, inv, all_pairs);
-          bool stop = false;
-          f_ranges(cend, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
-            for (int q = q0; q < q1 && !stop; ++q) {
-              const int rj = srank[q];
-              if (rj >= r) continue;
-              const unsigned char sj = st[rj];
-              if (sj == 2) continue;
-              const f32x4 o = sbox[q];
-              if (suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
-                if (sj == 1) { res = 2; stop = true; }
-                else res = 1;
-              }
-            }
-          });
-        }
-        if (res == 2) st[r] = 2;
-        else if (res == 0) st[r] = 1;
-        else undecided = 1;
-      }
-      if (undecided) s_flag = 1;
-      __syncthreads();
-      const int more = s_flag;
-      __syncthreads();
-#ifdef YCX_NMS_PROFILE
-      if (tid == 0) atomicAdd(&g_nms_wprof[5], 1ull);
-#endif
-      if (!more) break;
-    }
-    YCX_WPROF_MARK(3)
-    // (6) kept rows in rank order
-    int base = 0;
-    for (int r0 = 0; r0 < S; r0 += kBigThreads) {
-      const int r = r0 + tid;
-      const int k = (r < S && st[r] == 1) ? 1 : 0;
-      int total;
-      const int pos = block_exclusive(k, s_w, &total);
-      if (k) P.kept[off + base + pos] = bucket[r];
-      base += total;
-    }
-    if (tid == 0) P.kc[tk.cls] = base;
-    __syncthreads();
-    YCX_WPROF_MARK(4)
+  const BigList bl = big_list(ws, L, d.n);
+  for (int t = blockIdx.x; t < bl.size(); t += gridDim.x) {
+    if (t < bl.nwide) resolve_wide(L, ws, t, bl.wide[t], smem, s_lv, s_w, &s_flag, thr, t_lo, inv_t, all_pairs);
+    else resolve_fast(L, ws, t - bl.nwide, smem, s_lv, s_w, &s_flag, thr, t_lo, inv_t, all_pairs);
   }
 }
 
@@ -1949,8 +2288,8 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   // the 24 wide and 24 fast classes of a batch then run side by side instead of in turn
   // (YCX_NMS_NO_FAST: every class on the wide path, the fast list empty)
   hipLaunchKernelGGL(nms_fast<8>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs, 1);
-  hipLaunchKernelGGL(nms_wide_s, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
-  hipLaunchKernelGGL(nms_wide_b, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
+  hipLaunchKernelGGL(nms_search, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
+  hipLaunchKernelGGL(nms_resolve, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
   hipLaunchKernelGGL(nms_finish, dim3(d->n), dim3(kThreads), 0, st, *d, cand, ws, dets, keep_rows, keep_counts);
   return ycx_launch_status();
 }
