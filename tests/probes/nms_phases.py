@@ -25,7 +25,7 @@ def main():
     _, det, _, _, _ = bench.setup(args, dev, use_graph=False)
     det()
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * 24)()
+    buf = (ctypes.c_ulonglong * 32)()
     prof = hasattr(L.lib, "ycx_nms_prof_read")  # False on the release library: post time only
     if not prof:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -63,6 +63,8 @@ def main():
         print(f"  nms_wide: {wt // reps} tasks/step; " + "  ".join(
             f"{n} {buf[16 + i] / wt / 1e3:.1f}" for i, n in enumerate(PHASES)) + f" kcycles/task; rounds/task {buf[21] / wt:.1f}; "
               f"positions visited in rounds/task {buf[22] / wt:.0f}")
+        print(f"  wide sort: key build {buf[24] / wt / 1e3:.1f}  passes {buf[25] / wt / 1e3:.1f} kcycles/task over "
+              f"{buf[26] / wt:.1f} passes")
     cnt = det.counts.cpu()
     print("candidates/img", cnt.float().mean().item())
     ws = det.ws.view(torch.int32).cpu()  # header (ntasks) then the task table {img, cls, off, S} at byte 256

@@ -496,6 +496,12 @@ def test_nms_many_big_classes_unsplit(device):
     _check_keep(pred, 40, 0.0, 0.45)
 
 
+def test_nms_wide_class_past_u16_ranks(device):
+    """One class of 60k boxes: past the u16 rank range the wide path stages in LDS (~52.5k),
+    so its search and fixed point keep 16 int ranks per box and read the ranks from L2."""
+    _check_keep(_random_pred(1, 60000, 1, seed=19, size_lo=-2.0, size_hi=-1.0), 1, 0.0, 0.45)
+
+
 def test_nms_spatial_pixel_coords_and_clusters(device):
     # pixel units (class extent normalisation) and tight clusters of near-duplicates
     pred = _random_pred(1, 5000, 1, seed=12, scale=640.0, size_lo=-2.5, size_hi=-0.5)
@@ -546,7 +552,9 @@ def test_nms_big_class_score_ties(device):
     _check_keep(pred, 1, 0.0, 0.3)
     pred[..., 4] = 0.75  # one score for every box: the order is the row order alone
     _check_keep(pred, 1, 0.0, 0.3)
-    wide = _random_pred(1, 20000, 1, seed=17, size_lo=-2.5, size_hi=-1.5)  # nms_wide's global radix sort
-    wide[..., 4] = 0.5 + 0.0625 * torch.randint(0, 8, (1, 20000), generator=g).float()
+    wide = _random_pred(1, 20000, 1, seed=17, size_lo=-2.5, size_hi=-1.5)  # a wide class: bins of ~2500
+    wide[..., 4] = 0.5 + 0.0625 * torch.randint(0, 8, (1, 20000), generator=g).float()  # ties: the radix sort
     wide[..., 5] = 1.0
+    _check_keep(wide, 1, 0.0, 0.3)
+    wide[..., 4] = 0.75  # one score: the keys differ in the row bits only, the bin rank orders by row
     _check_keep(wide, 1, 0.0, 0.3)

@@ -1,6 +1,6 @@
-// Per-image, per-class greedy NMS with torchvision.ops.nms semantics — the
+// Per-image, per-class greedy NMS with torchvision.ops.nms semantics -- the
 // loop of detect.py:124-137 (unique classes ascending, nms per class, results
-// concatenated class by class) for the whole batch in three launches.
+// concatenated class by class) for the whole batch in seven launches.
 //
 //  nms_count / nms_bucket / nms_prep   16 workgroups per image: class histograms
 //              of candidate slices, exclusive scan -> one bucket per class; every
@@ -8,23 +8,27 @@
 //              candidates is finished entirely in registers (64*R keys
 //              bitonic-sorted across lanes and register slots, greedy scan with
 //              removed/kept bit masks, box i broadcast by readlane). Larger
-//              classes are queued as tasks (nms_fast / nms_wide, below; the r02
-//              general path nms_big is retired: tools/experiments/nms_big_r02.patch).
-//  (r02 design, kept by nms_fast / nms_wide) one 1024-thread workgroup per large
-//              class (grid-strided task loop). (1) score sort (score desc, row asc = torchvision's stable
-//              descending order) -> rank. (2) spatial counting sort: level =
-//              size octave of max(w, h) relative to the class extent, cell =
-//              centre cell in a 2^L x 2^L grid of that level. (3) per box, the
-//              higher-ranked boxes with IoU > thr ("suppressors") are searched
-//              only where they can exist: IoU > t forces w_j/w_i and h_j/h_i
-//              into (t, 1/t) (so only a few levels qualify) and the boxes to
-//              overlap (so only the cells whose centres lie within half the
-//              level's largest box of this one). (4) greedy resolution as a
-//              parallel fixed point: a box is kept once all its suppressors are
-//              removed, removed once any is kept; every round decides at least
-//              the highest-ranked undecided box, and each decision equals the
-//              greedy one by induction on rank. (5) kept rows compacted in rank
-//              order.
+//              classes are listed: the fast list (the class fits the LDS) and the
+//              wide list (the others).
+//  A big class, one 1024-thread workgroup per phase (grid-strided task loops):
+//              (1) score sort (score desc, row asc = torchvision's stable descending
+//              order) -> rank. (2) spatial counting sort: level = size octave of
+//              max(w, h) relative to the class extent, cell = centre cell in that
+//              level's grid. (3) per box, the higher-ranked boxes with IoU > thr
+//              ("suppressors") are searched only where they can exist: IoU > t
+//              forces w_j/w_i and h_j/h_i into (t, 1/t) (so only a few levels
+//              qualify) and the centres within a window the sizes bound. (4) greedy
+//              resolution as a parallel fixed point: a box is kept once all its
+//              suppressors are removed, removed once any is kept; every round
+//              decides at least the highest-ranked undecided box, and each decision
+//              equals the greedy one by induction on rank. (5) kept rows compacted
+//              in rank order.
+//  nms_fast    (1)-(2) of every class; a fast class also (3)-(5) in LDS, unless the
+//              batch has few big classes (kSplitTasks), when it is split like the
+//              wide ones.
+//  nms_search  (3) of the wide and split classes, their positions spread evenly
+//              over the grid.
+//  nms_resolve (4)-(5) of the wide and split classes.
 //  nms_finish  one workgroup per image: exclusive scan of the per-class kept
 //              counts places every kept row in class order; padded outputs.
 //
@@ -40,7 +44,7 @@
 namespace {
 
 constexpr int kThreads = 1024;
-// nms_big's workgroup, LDS budget and grid (build-time knobs, DESIGN.md §6 tried-and-rejected)
+// the big-class kernels' workgroup, LDS budget and grid (build-time knobs, DESIGN.md §6 tried-and-rejected)
 #ifndef YCX_NMS_BIG_THREADS
 #define YCX_NMS_BIG_THREADS 1024
 #endif
@@ -56,18 +60,13 @@ constexpr int kMaxRows = 131072;  // rows (candidates) per image
 #define YCX_NMS_BIG_BLOCKS 256
 #endif
 constexpr int kBigBlocks = YCX_NMS_BIG_BLOCKS;   // nms_fast / nms_wide grid (task-strided)
-constexpr int kSlots = 16;        // highest-ranked suppressors cached per box
-#ifndef YCX_NMS_LEVELS
-#define YCX_NMS_LEVELS 7
-#endif
-constexpr int kLevels = YCX_NMS_LEVELS;  // size octaves: level L holds max(w, h) < 2^-L of the class extent
-constexpr int kGridCells = ((1 << (2 * kLevels)) - 1) / 3;  // sum_{L < kLevels} 4^L
-constexpr int kWild = kGridCells; // one extra cell: boxes without a finite positive size
+constexpr int kSlots = 16;        // int suppressor ranks cached per box (64 bytes; 32 when u16)
 
 #ifdef YCX_NMS_PROFILE
-// Development counters: shader cycles per nms_big phase, summed over tasks.
+// Development counters: shader cycles per big-class phase, summed over tasks.
 __device__ unsigned long long g_nms_prof[16];
-__device__ unsigned long long g_nms_wprof[8];  // nms_wide: phases 0-4, [5] rounds, [7] tasks
+__device__ unsigned long long g_nms_wprof[16];  // wide: phases 0-4, [5] rounds, [6] round visits, [7] tasks,
+                                               // [8] sort key build, [9] sort passes, [10] pass count
 #define YCX_PROF_MARK(i)                                               \
   if (tid == 0) {                                                      \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime();      \
@@ -318,87 +317,6 @@ __device__ int wave_exclusive_scan(const int* in, int* out, int n) {
   return __shfl(incl, 63);
 }
 
-__device__ void block_bitonic(unsigned long long* keys, int P) {
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < P; i += blockDim.x) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const unsigned long long x = keys[i], y = keys[ixj];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) { keys[i] = y; keys[ixj] = x; }
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-// Workgroup bitonic sort of Pn = E * kThreads keys held in registers (element
-// e = tid*E + i): partners within a thread are exchanged in registers, within
-// a wave by shuffles, and only the strides that cross waves go through LDS.
-template <int E>
-__device__ void sort_regs(unsigned long long (&v)[E], unsigned long long* lds, int Pn) {
-  const int t = threadIdx.x;
-  for (int k = 2; k <= Pn; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j < E) {
-#pragma unroll
-        for (int jj = E / 2; jj >= 1; jj >>= 1) {
-          if (jj != j) continue;
-#pragma unroll
-          for (int i = 0; i < E; ++i) {
-            if (i & jj) continue;
-            const int ip = i | jj;
-            const bool up = ((t * E + i) & k) == 0;
-            const unsigned long long a = v[i], b = v[ip];
-            if ((a > b) == up) { v[i] = b; v[ip] = a; }
-          }
-        }
-      } else if (j < 64 * E) {
-        const int lj = j / E;
-#pragma unroll
-        for (int i = 0; i < E; ++i) {
-          const int e = t * E + i;
-          const unsigned long long o = __shfl_xor(v[i], lj);
-          const bool up = (e & k) == 0, lower = (e & j) == 0;
-          const unsigned long long mn = v[i] < o ? v[i] : o, mx = v[i] < o ? o : v[i];
-          v[i] = (lower == up) ? mn : mx;
-        }
-      } else {
-        __syncthreads();  // the previous exchange's reads are done
-#pragma unroll
-        for (int i = 0; i < E; ++i) lds[t * E + i] = v[i];
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < E; ++i) {
-          const int e = t * E + i;
-          const unsigned long long o = lds[e ^ j];
-          const bool up = (e & k) == 0, lower = (e & j) == 0;
-          const unsigned long long mn = v[i] < o ? v[i] : o, mx = v[i] < o ? o : v[i];
-          v[i] = (lower == up) ? mn : mx;
-        }
-      }
-    }
-  }
-}
-
-// Sort the keys of one class (bucket order in, rank order out in lds[0, Pn)).
-template <int E>
-__device__ void sort_class(const ycx_cand* __restrict__ ci, const int* bucket, int S, unsigned long long* lds) {
-  unsigned long long v[E];
-#pragma unroll
-  for (int i = 0; i < E; ++i) {
-    const int e = threadIdx.x * E + i;
-    v[i] = e < S ? make_key(ci[bucket[e]]) : ~0ull;
-  }
-  sort_regs<E>(v, lds, E * (int)blockDim.x);
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < E; ++i) lds[threadIdx.x * E + i] = v[i];
-  __syncthreads();
-}
-
 struct Ptrs {
   unsigned long long* keys;
   int *bucket, *kept;
@@ -542,7 +460,7 @@ __global__ void __launch_bounds__(kThreads) nms_prep(ycx_nms_desc d, const ycx_c
 }
 
 // ---------------------------------------------------------------------------
-// nms_big helpers
+// big-class helpers
 
 // Order-preserving int image of a float (LDS atomicMin/Max on floats).
 __device__ __forceinline__ int f2o(float f) {
@@ -551,250 +469,13 @@ __device__ __forceinline__ int f2o(float f) {
 }
 __device__ __forceinline__ float o2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
 
-__device__ __forceinline__ int level_base(int L) { return ((1 << (2 * L)) - 1) / 3; }  // sum_{l < L} 4^l
-
 __device__ __forceinline__ int clamp_cell(float v, int G) {
   return (int)fminf(fmaxf(floorf(v), 0.0f), (float)(G - 1));
 }
 
-// Class-normalised geometry of one box: level = size octave of max(w, h),
-// cell = centre cell of that level's 2^L x 2^L grid; level -1 = irregular
-// (non-finite or non-positive extent: compared against every box).
-struct Geo {
-  float nx1, ny1, nx2, ny2, w, h;
-  int level, cell;
-};
-
-__device__ __forceinline__ Geo geometry(const f32x4 b, float X0, float Y0, float inv, bool all_pairs) {
-  Geo g;
-  g.nx1 = (b[0] - X0) * inv;
-  g.ny1 = (b[1] - Y0) * inv;
-  g.nx2 = (b[2] - X0) * inv;
-  g.ny2 = (b[3] - Y0) * inv;
-  g.w = g.nx2 - g.nx1;
-  g.h = g.ny2 - g.ny1;
-  const float s = fmaxf(g.w, g.h);
-  const bool reg = !all_pairs && g.w > 0.0f && g.h > 0.0f && s < INFINITY && b[0] > -INFINITY && b[1] > -INFINITY;
-  if (!reg) {
-    g.level = -1;
-    g.cell = kWild;
-    return g;
-  }
-  const int e = (int)(__float_as_uint(s) >> 23) - 126;  // s < 2^e
-  const int L = min(max(-e, 0), kLevels - 1);
-  const int G = 1 << L;
-  const int ix = clamp_cell((g.nx1 + g.nx2) * 0.5f * (float)G, G);
-  const int iy = clamp_cell((g.ny1 + g.ny2) * 0.5f * (float)G, G);
-  g.level = L;
-  g.cell = level_base(L) + iy * G + ix;
-  return g;
-}
-
-// Spatially sorted boxes of one large class: in LDS (ranks as u16) when they
-// fit, else in the per-image workspace.
-template <bool kLds>
-struct Ctx {
-  const int* cells;  // LDS: end position of cell k (start = cells[k - 1], 0 for k = 0)
-  const int (*lv)[5];  // LDS: per level count, max w, max h, min w, min h (float bits)
-  const f32x4* sbox;
-  const unsigned short* r16;
-  const int* r32;
-  float t_lo, inv_t;
-  int S;
-  __device__ __forceinline__ int rank(int q) const {
-    if constexpr (kLds) return r16[q];
-    else return r32[q];
-  }
-};
-
 // (x2 - x1) * (y2 - y1): the reference's area expression, bit-identical to the
 // one the candidates were filtered with (contraction is off in this file).
 __device__ __forceinline__ float box_area(const f32x4 b) { return (b[2] - b[0]) * (b[3] - b[1]); }
-
-// The position ranges (cell rows of the compatible levels) that can hold a box
-// with IoU > thr against the box of geometry g; run(q0, q1) returns false to
-// stop. IoU > t forces t < w_j/w_i < 1/t and t < h_j/h_i < 1/t (IoU <= inter/a_j <=
-// w_i h_j/(w_j h_j)) and overlap (centre within half the partner's extent).
-// The ratio tests use t_lo = t(1 - 1e-3) and an absolute slack, the windows a
-// 1e-5 margin, both far above the fp32 rounding of the normalised geometry.
-template <bool kLds, class F>
-__device__ __forceinline__ bool for_ranges(const Ctx<kLds>& c, const Geo& g, F&& run) {
-  if (g.level < 0) return run(0, c.S);
-  if (!run(c.cells[kWild - 1], c.cells[kWild])) return false;
-  constexpr float kSlack = 1e-6f, kEps = 1e-5f;
-  for (int L = 0; L < kLevels; ++L) {
-    if (c.lv[L][0] == 0) continue;
-    const float mw = __int_as_float(c.lv[L][1]), mh = __int_as_float(c.lv[L][2]);
-    const float nw = __int_as_float(c.lv[L][3]), nh = __int_as_float(c.lv[L][4]);
-    if (mw + kSlack < c.t_lo * g.w || mh + kSlack < c.t_lo * g.h) continue;  // all too narrow / too flat
-    if (nw - kSlack > (g.w + kSlack) * c.inv_t || nh - kSlack > (g.h + kSlack) * c.inv_t) continue;  // too big
-    const int G = 1 << L, base = level_base(L);
-    const float Gf = (float)G;
-    const int ix0 = clamp_cell((g.nx1 - 0.5f * mw - kEps) * Gf, G), ix1 = clamp_cell((g.nx2 + 0.5f * mw + kEps) * Gf, G);
-    const int iy0 = clamp_cell((g.ny1 - 0.5f * mh - kEps) * Gf, G), iy1 = clamp_cell((g.ny2 + 0.5f * mh + kEps) * Gf, G);
-    for (int iy = iy0; iy <= iy1; ++iy) {  // cells ix0..ix1 of a grid row are contiguous positions
-      const int k0 = base + iy * G + ix0, k1 = base + iy * G + ix1;
-      if (!run(k0 ? c.cells[k0 - 1] : 0, c.cells[k1])) return false;
-    }
-  }
-  return true;
-}
-
-// Visit every spatial position q whose box can have IoU > thr with the box of
-// geometry g (for_ranges) and whose rank is below r; f(q, rank) returns false
-// to stop.
-template <bool kLds, class F>
-__device__ __forceinline__ bool for_candidates(const Ctx<kLds>& c, const Geo& g, int r, F&& f) {
-  return for_ranges(c, g, [&](int q0, int q1) -> bool {
-    for (int q = q0; q < q1; ++q) {
-      const int rj = c.rank(q);
-      if (rj < r && !f(q, rj)) return false;
-    }
-    return true;
-  });
-}
-
-struct Frame {  // per-task values shared by the resolve phases
-  int S, off;
-  float X0, Y0, inv;
-  int all_pairs;
-};
-
-// Phases (4) suppressor search and (5) fixed-point resolution of one class.
-template <bool kLds>
-__device__ void resolve(const Ctx<kLds>& c, const Frame& fr, const Ptrs& P, unsigned char* st, const Thr& thr,
-                        int* s_flag) {
-  const int tid = threadIdx.x, S = fr.S, off = fr.off;
-#ifdef YCX_NMS_PROFILE
-  unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
-#endif
-  // (4) suppressors of every box (spatial order: a wave's boxes share level and
-  // neighbourhood). Each box keeps its kSlots highest-ranked suppressors
-  // (smallest ranks, ascending): they decide most boxes, and a box needs a
-  // rescan only when all of them end up removed while more exist.
-  for (int p = tid; p < S; p += kBigThreads) {
-    const int r = c.rank(p);
-    const f32x4 b = c.sbox[p];
-    const float a = box_area(b);
-    const Geo g = geometry(b, fr.X0, fr.Y0, fr.inv, fr.all_pairs);
-    // the box's kSlots highest-ranked suppressors (unordered: appended while the
-    // list has room, then the lowest-ranked replaced) and their total count; a box
-    // needs a rescan only when the cached ones all end up removed while more exist
-    int* sl = P.slots + (size_t)(off + p) * kSlots;
-    int ns = 0;
-#ifdef YCX_NMS_PROFILE
-    int visits = 0;
-#endif
-    auto test = [&](int rj, const f32x4& o) {
-      // for thr >= 0 a suppressor must overlap (inter > 0): four compares first
-      const bool cand = rj < r && (fr.all_pairs || (o[0] < b[2] && o[2] > b[0] && o[1] < b[3] && o[3] > b[1]));
-      if (cand && suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
-        if (ns < kSlots) {
-          sl[ns] = rj;
-        } else {  // rare (a few % of the boxes): keep the kSlots highest-ranked (smallest ranks)
-          int km = 0, vm = sl[0];
-          for (int k = 1; k < kSlots; ++k) {
-            const int v = sl[k];
-            if (v > vm) { vm = v; km = k; }
-          }
-          if (rj < vm) sl[km] = rj;
-        }
-        ++ns;
-      }
-    };
-    for_ranges(c, g, [&](int q0, int q1) {
-#ifdef YCX_NMS_PROFILE
-      visits += q1 - q0;
-#endif
-      int q = q0;
-      for (; q + 4 <= q1; q += 4) {  // four candidates' loads in flight
-        int rj[4];
-        f32x4 o[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          rj[u] = c.rank(q + u);
-          o[u] = c.sbox[q + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) test(rj[u], o[u]);
-      }
-      for (; q < q1; ++q) test(c.rank(q), c.sbox[q]);
-      return true;
-    });
-    P.nsup[off + p] = ns;
-#ifdef YCX_NMS_PROFILE
-    if (ns > kSlots) atomicAdd(&g_nms_prof[6], 1ull);
-    atomicAdd(&g_nms_prof[8], (unsigned long long)visits);
-    atomicAdd(&g_nms_prof[10], (unsigned long long)ns);
-    int mx = visits;
-    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
-    if ((tid & 63) == 0) atomicAdd(&g_nms_prof[9], (unsigned long long)mx);
-#endif
-  }
-  // (5) greedy as a fixed point over ranks: 0 undecided, 1 kept, 2 removed
-  for (int r = tid; r < S; r += kBigThreads) st[r] = 0;
-  __syncthreads();
-  YCX_PROF_MARK(2)
-  for (int it = 0; it <= S; ++it) {  // every round decides at least one box
-    if (tid == 0) *s_flag = 0;
-    __syncthreads();
-    int undecided = 0;
-    for (int p = tid; p < S; p += kBigThreads) {
-      const int r = c.rank(p);
-      if (st[r] != 0) continue;
-      const int ns = P.nsup[off + p];
-      int res = 0;  // 0: every suppressor removed, 1: some undecided, 2: one kept
-      // the box's cached suppressors in one 64-byte read (one memory round trip per box
-      // and round instead of one per suppressor); entries past ns are never looked at
-      const int4* sl4 = reinterpret_cast<const int4*>(P.slots + (size_t)(off + p) * kSlots);
-      int sl[kSlots];
-#pragma unroll
-      for (int q = 0; q < kSlots / 4; ++q) {
-        const int4 v = sl4[q];
-        sl[4 * q] = v.x;
-        sl[4 * q + 1] = v.y;
-        sl[4 * q + 2] = v.z;
-        sl[4 * q + 3] = v.w;
-      }
-      const int nc_ = min(ns, kSlots);
-#pragma unroll
-      for (int k = 0; k < kSlots; ++k) {
-        if (k < nc_ && res != 2) {
-          const unsigned char sj = st[sl[k]];
-          if (sj == 1) res = 2;
-          else if (sj == 0) res = 1;
-        }
-      }
-      if (ns > kSlots && res == 0) {  // the cached ones are all removed: look at the rest
-        const f32x4 b = c.sbox[p];
-        const float a = box_area(b);
-        const Geo g = geometry(b, fr.X0, fr.Y0, fr.inv, fr.all_pairs);
-        for_candidates(c, g, r, [&](int q, int rj) {
-          const unsigned char sj = st[rj];
-          if (sj == 2) return true;
-          const f32x4 o = c.sbox[q];
-          if (suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
-            if (sj == 1) { res = 2; return false; }
-            res = 1;
-          }
-          return true;
-        });
-      }
-      if (res == 2) st[r] = 2;
-      else if (res == 0) st[r] = 1;
-      else undecided = 1;
-    }
-    if (undecided) *s_flag = 1;
-    __syncthreads();
-    const int more = *s_flag;
-    __syncthreads();
-#ifdef YCX_NMS_PROFILE
-    if (tid == 0) atomicAdd(&g_nms_prof[5], 1ull);
-#endif
-    if (!more) break;
-  }
-  YCX_PROF_MARK(3)
-}
 
 // Block-wide exclusive scan helper: returns this thread's exclusive prefix of
 // `v` over the workgroup and writes the block total to *total.
@@ -820,7 +501,7 @@ __device__ __forceinline__ int block_exclusive(int v, int* s_w, int* total) {
 }
 
 // ---------------------------------------------------------------------------
-// nms_big fast path: a class of S <= kFastMax boxes held entirely in LDS.
+// The fast path: a class of S <= kFastMax boxes held entirely in LDS.
 // Same greedy semantics and the same suppressor / fixed-point logic as the
 // general path (resolve), with three changes that cut the per-class cost:
 //  * every candidate is gathered from global memory ONCE (into registers), and
@@ -965,6 +646,54 @@ __device__ __forceinline__ FGeo fgeometry(const f32x4 b, float X0, float Y0, flo
   return g;
 }
 
+// Per-level box count and extreme sizes (float bits: the sizes are non-negative), summed per
+// thread in registers over all its boxes, then wave-reduced into s_lv with one set of LDS
+// atomics per wave and level (instead of a ballot and four reductions per box and level).
+struct LevelStats {
+  int n[kFLevels], mxw[kFLevels], mxh[kFLevels], mnw[kFLevels], mnh[kFLevels];
+  __device__ __forceinline__ LevelStats() {
+#pragma unroll
+    for (int L = 0; L < kFLevels; ++L) {
+      n[L] = 0;
+      mxw[L] = mxh[L] = 0;
+      mnw[L] = mnh[L] = 0x7F800000;
+    }
+  }
+  __device__ __forceinline__ void add(const FGeo& g) {
+#pragma unroll
+    for (int L = 0; L < kFLevels; ++L) {
+      if (g.level == L) {
+        ++n[L];
+        mxw[L] = max(mxw[L], __float_as_int(g.w));
+        mxh[L] = max(mxh[L], __float_as_int(g.h));
+        mnw[L] = min(mnw[L], __float_as_int(g.w));
+        mnh[L] = min(mnh[L], __float_as_int(g.h));
+      }
+    }
+  }
+  __device__ __forceinline__ void flush(int (*s_lv)[5]) {
+#pragma unroll
+    for (int L = 0; L < kFLevels; ++L) {
+      int c = n[L], a = mxw[L], b = mxh[L], e = mnw[L], f = mnh[L];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_xor(c, o);
+        a = max(a, __shfl_xor(a, o));
+        b = max(b, __shfl_xor(b, o));
+        e = min(e, __shfl_xor(e, o));
+        f = min(f, __shfl_xor(f, o));
+      }
+      if ((threadIdx.x & 63) == 0 && c > 0) {
+        atomicAdd(&s_lv[L][0], c);
+        atomicMax(&s_lv[L][1], a);
+        atomicMax(&s_lv[L][2], b);
+        atomicMin(&s_lv[L][3], e);
+        atomicMin(&s_lv[L][4], f);
+      }
+    }
+  }
+};
+
 // max over w_j in [nw, mw] of (w_i + w_j) / 2 - t max(w_i, w_j): the largest centre
 // distance at which a partner of that width range can still pass IoU > t
 __device__ __forceinline__ float reach(float wi, float nw, float mw, float t) {
@@ -1009,6 +738,10 @@ __device__ __forceinline__ void f_ranges(CE&& cend, const int (*lv)[5], const FG
 // one 64-byte read, so a box rarely needs a rescan and the search never walks a
 // dependent chain of global loads.
 constexpr int kFSlots = 32;
+// classes up to this size keep u16 slots (wide ones too) and stage their u16 ranks in LDS beside
+// the u32 cell ends for the search (nms_search); larger ones keep 16 int slots
+constexpr int kSlot16Max = (kBigLds - (((kFCells * 4) + 15) & ~15)) / 2;
+static_assert(kSlot16Max <= 65535, "u16 ranks");
 
 // f(k, v) for the first c of a box's u16 slots, read as 16-byte chunks (4 registers live)
 template <class F>
@@ -1021,6 +754,26 @@ __device__ __forceinline__ void for_slots16(const unsigned short* sl, int c, F&&
     for (int h = 0; h < 8; ++h)
       if (8 * q + h < c) f(8 * q + h, (int)(((unsigned)w[h >> 1] >> (16 * (h & 1))) & 0xFFFFu));
   }
+}
+
+// The combined state of a box's cached suppressors csr[b0 .. b0 + c): 2 if one is kept, else
+// 1 if one is undecided, else 0 (all removed). Four ranks, then their four states, are read
+// together (no read waits on the previous state); the scan stops once one is kept.
+__device__ __forceinline__ int csr_state(const unsigned short* csr, int b0, int c, const unsigned char* st) {
+  int res = 0;
+  for (int k = 0; k < c && res != 2; k += 4) {
+    int v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = k + u < c ? (int)csr[b0 + k + u] : -1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (v[u] >= 0) {
+        const unsigned char sj = st[v[u]];
+        res = max(res, sj == 1 ? 2 : (sj == 0 ? 1 : 0));
+      }
+    }
+  }
+  return res;
 }
 
 // the rare replacement past kFSlots: keep the kFSlots highest-ranked (smallest ranks)
@@ -1061,11 +814,7 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
   // (2) rank sort in registers (exchange through LDS), then every element learns its rank
   unsigned long long* xch = reinterpret_cast<unsigned long long*>(smem);
   unsigned short* rank_of = reinterpret_cast<unsigned short*>(smem + 8 * kFastMax);
-#ifdef YCX_NMS_BITONIC  // development A/B: the bitonic sort of the general path
-  sort_regs<E>(key, xch, E * kBigThreads);
-#else
   radix_sort_regs<E>(key, S, 13, xch, reinterpret_cast<unsigned short*>(smem + 10 * kFastMax), s_w, s_msk);
-#endif
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < E; ++i)
@@ -1134,33 +883,12 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
       atomicAdd(&cells[k >> 1], 1u << ((k & 1) * 16));
     }
   }
-  // per-level count / extreme sizes: wave-reduced, one LDS atomic per wave and level
+  {  // per-level count / extreme sizes
+    LevelStats ls;
 #pragma unroll
-  for (int i = 0; i < E; ++i) {
-    FGeo g;
-    g.level = -1;
-    if (tid * E + i < S) g = fgeometry(box[i], X0, Y0, inv, all_pairs);
-    for (int Lv = 0; Lv < kFLevels; ++Lv) {
-      const bool in = g.level == Lv;
-      const unsigned long long m = __ballot(in);
-      if (!m) continue;
-      int mxw = in ? __float_as_int(g.w) : 0, mxh = in ? __float_as_int(g.h) : 0;
-      int mnw = in ? __float_as_int(g.w) : 0x7F800000, mnh = in ? __float_as_int(g.h) : 0x7F800000;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        mxw = max(mxw, __shfl_xor(mxw, o));
-        mxh = max(mxh, __shfl_xor(mxh, o));
-        mnw = min(mnw, __shfl_xor(mnw, o));
-        mnh = min(mnh, __shfl_xor(mnh, o));
-      }
-      if (lane == 0) {
-        atomicAdd(&s_lv[Lv][0], __popcll(m));
-        atomicMax(&s_lv[Lv][1], mxw);
-        atomicMax(&s_lv[Lv][2], mxh);
-        atomicMin(&s_lv[Lv][3], mnw);
-        atomicMin(&s_lv[Lv][4], mnh);
-      }
-    }
+    for (int i = 0; i < E; ++i)
+      if (tid * E + i < S) ls.add(fgeometry(box[i], X0, Y0, inv, all_pairs));
+    ls.flush(s_lv);
   }
   __syncthreads();
   {  // exclusive scan of the u16 counts, in place: each thread a contiguous run of cells
@@ -1326,11 +1054,7 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
       int ns, res = 0;  // 0: every suppressor removed, 1: some undecided, 2: one kept
       if (lds_csr) {
         ns = csr_ns[p];
-        const int b0 = csr_off[p], c = min(ns, kFSlots);
-        for (int k = 0; k < c && res != 2; ++k) {
-          const unsigned char sj = st[csr[b0 + k]];
-          res = sj == 1 ? 2 : (sj == 0 ? 1 : res);
-        }
+        res = csr_state(csr, (int)csr_off[p], min(ns, kFSlots), st);
       } else {
         ns = P.nsup[off + p];
         for_slots16(reinterpret_cast<const unsigned short*>(P.slots + (size_t)(off + p) * kSlots), min(ns, kFSlots),
@@ -1390,7 +1114,7 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
 
 // ---------------------------------------------------------------------------
 // The LDS-resident classes (S <= kFastMax and fast_lds_bytes(S) fits): big_fast, one
-// 1024-thread workgroup per class (grid-strided task loop); nms_big then takes the rest.
+// 1024-thread workgroup per class (grid-strided task loop), beside the wide classes' sort and index.
 __device__ __forceinline__ void wide_a_task(const ycx_nms_desc& d, const ycx_cand* __restrict__ cand, char* ws,
                                             const Layout& L, int t, const Task& tk, char* smem, int (*s_lv)[5],
                                             int* s_ext, int* s_w, unsigned long long* s_msk, int all_pairs);
@@ -1416,7 +1140,8 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   for (int w = blockIdx.x; w < nwide + ntasks; w += gridDim.x) {
     if (w < nwide) {
       constexpr int kCellB = ((kFCells * 4) + 255) & ~255;  // u32 cell ends
-      static_assert(kBigLds >= 16 * (kMaxRows / kBigThreads) * (kBigThreads / 64) * 4 && kBigLds >= kCellB + 1024,
+      static_assert(kBigLds >= 16 * (kMaxRows / kBigThreads) * (kBigThreads / 64) * 4 &&
+                        kBigLds >= 64 * 32 * (kBigThreads / 64) * 4 && kBigLds >= kCellB + 1024,
                     "wide path LDS: radix counts, cells");
       const Task* wt = tasks + (size_t)d.n * L.max_tasks;  // the wide list
       wide_a_task(d, cand, ws, L, w, wt[w], smem, s_lv, s_ext, s_w, s_msk, all_pairs);
@@ -1476,34 +1201,41 @@ __device__ __forceinline__ void replace_slot32(int* sl, int rj) {  // keep the k
   if (rj < vm) sl[km] = rj;
 }
 
-// Stable LSD rank sort (4-bit digits, digits every key shares skipped) of a wide class's S
+// Stable LSD rank sort (B-bit digits, digits every key shares skipped) of a wide class's S
 // keys (score desc, row asc) in global scratch. Striped layout (coalesced): element p = i *
 // kBigThreads + tid, i < E = ceil(S / kBigThreads) <= 128. A pass counts, per (digit, i, wave),
-// the wave's elements of slot i with that digit (the lanes with equal digits found by four
+// the wave's elements of slot i with that digit (the lanes with equal digits found by B
 // ballots), scans the counts in (digit, i, wave) order -- the input order within each digit --
 // and scatters every key to its count's offset plus its rank among the equal-digit lanes below
 // it: stable, and the lanes of a group write consecutive addresses. Keys move in batches of 8
 // slots per thread with the batch's loads issued together (one memory round trip per 8 keys,
 // not per key); the last pass scatters the rows themselves into bucket (rank order).
-// a / b: 8 S bytes each; C: LDS u32 [16][E][16] (<= 128 KiB).
+// a / b: 8 S bytes each; C: LDS u32 [2^B][E][16] (<= 128 KiB: B = 6 up to E = 32, else 4).
+template <int B>
 __device__ __forceinline__ unsigned long long same_digit_lanes(int dg) {
   unsigned long long m = ~0ull;
 #pragma unroll
-  for (int bit = 0; bit < 4; ++bit) {
+  for (int bit = 0; bit < B; ++bit) {
     const unsigned long long bl = __ballot((dg >> bit) & 1);
     m &= ((dg >> bit) & 1) ? bl : ~bl;
   }
   return m;
 }
 
+template <int B>  // digit bits
 __device__ void radix_rank(const ycx_cand* __restrict__ ci, int* bucket, int S, unsigned long long* a,
                            unsigned long long* b, unsigned* C, int* s_w, unsigned long long* s_msk) {
+  constexpr int D = 1 << B;
+  constexpr unsigned long long DM = D - 1;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int NW = kBigThreads / 64;
   const int E = (S + kBigThreads - 1) / kBigThreads;
   const int nch = (E + 7) / 8;  // uniform
   const unsigned long long lt = (1ull << lane) - 1ull;  // lanes below this one
   auto at = [&](int c, int j) { return (8 * c + j) * kBigThreads + tid; };
+#ifdef YCX_NMS_PROFILE
+  const unsigned long long t_sort0 = __builtin_amdgcn_s_memtime();
+#endif
   unsigned long long an = ~0ull, orr = 0ull;
   for (int c = 0; c < nch; ++c) {  // keys built from the candidates into a
     int row[8];
@@ -1533,11 +1265,15 @@ __device__ void radix_rank(const ycx_cand* __restrict__ ci, int* bucket, int S, 
   __syncthreads();
   const unsigned long long diff = s_msk[0] ^ s_msk[1];
   int last = -1;  // the last digit any two keys differ in (none: S == 1, bucket already in order)
-  for (int sh = 0; sh < 64; sh += 4)
-    if ((diff >> sh) & 0xF) last = sh;
-  const int nC = 16 * E * NW;
-  for (int sh = 0; sh <= last; sh += 4) {
-    if (((diff >> sh) & 0xF) == 0) continue;  // uniform
+  for (int sh = 0; sh < 64; sh += B)
+    if ((diff >> sh) & DM) last = sh;
+  const int nC = D * E * NW;
+#ifdef YCX_NMS_PROFILE
+  unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
+  if (tid == 0) atomicAdd(&g_nms_wprof[8], t_prev_ - t_sort0);
+#endif
+  for (int sh = 0; sh <= last; sh += B) {
+    if (((diff >> sh) & DM) == 0) continue;  // uniform
     for (int c = tid; c < nC; c += kBigThreads) C[c] = 0;
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
@@ -1549,8 +1285,8 @@ __device__ void radix_rank(const ycx_cand* __restrict__ ci, int* bucket, int S, 
         const int i = 8 * c + j;
         if (i >= E) break;  // uniform: the ballots need every lane
         const bool ok = at(c, j) < S;
-        const int dg = ok ? (int)((k[j] >> sh) & 0xF) : 16;  // 16: past the end (matches no digit)
-        const unsigned long long m = same_digit_lanes(dg & 15) & __ballot(ok);
+        const int dg = ok ? (int)((k[j] >> sh) & DM) : D;  // D: past the end (matches no digit)
+        const unsigned long long m = same_digit_lanes<B>(dg & (D - 1)) & __ballot(ok);
         if (ok && (m & lt) == 0) C[(dg * E + i) * NW + wid] = (unsigned)__popcll(m);  // the group's first lane
       }
     }
@@ -1578,8 +1314,8 @@ __device__ void radix_rank(const ycx_cand* __restrict__ ci, int* bucket, int S, 
         const int i = 8 * c + j;
         if (i >= E) break;
         const bool ok = at(c, j) < S;
-        const int dg = ok ? (int)((k[j] >> sh) & 0xF) : 16;
-        const unsigned long long m = same_digit_lanes(dg & 15) & __ballot(ok);
+        const int dg = ok ? (int)((k[j] >> sh) & DM) : D;
+        const unsigned long long m = same_digit_lanes<B>(dg & (D - 1)) & __ballot(ok);
         if (ok) {
           const unsigned q = C[(dg * E + i) * NW + wid] + (unsigned)__popcll(m & lt);
           if (fin) bucket[q] = (int)(unsigned)k[j];
@@ -1591,7 +1327,13 @@ __device__ void radix_rank(const ycx_cand* __restrict__ ci, int* bucket, int S, 
     unsigned long long* t = a;
     a = b;
     b = t;
+#ifdef YCX_NMS_PROFILE
+    if (tid == 0) atomicAdd(&g_nms_wprof[10], 1ull);
+#endif
   }
+#ifdef YCX_NMS_PROFILE
+  if (tid == 0) atomicAdd(&g_nms_wprof[9], __builtin_amdgcn_s_memtime() - t_prev_);
+#endif
 }
 
 // nms_wide_a's work for wide task t: the class's keys sorted, boxes in rank order, the
@@ -1622,7 +1364,10 @@ __device__ __forceinline__ void wide_a_task(const ycx_nms_desc& d, const ycx_can
     }
     // (1) keys (score desc, row asc), radix-sorted: rank r = position; bucket in rank order
     unsigned long long* ka = P.keys + 2 * (size_t)off;
-    radix_rank(ci, bucket, S, ka, ka + S, reinterpret_cast<unsigned*>(smem), s_w, s_msk);
+    if (S <= 32 * kBigThreads)  // 6-bit digits while the count table (64 x E x 16 u32) fits the LDS
+      radix_rank<6>(ci, bucket, S, ka, ka + S, reinterpret_cast<unsigned*>(smem), s_w, s_msk);
+    else
+      radix_rank<4>(ci, bucket, S, ka, ka + S, reinterpret_cast<unsigned*>(smem), s_w, s_msk);
     __syncthreads();
     YCX_WPROF_MARK(0)
     // (2) boxes in rank order (the dead keys' region, 16 B per rank) and the class extent
@@ -1673,46 +1418,26 @@ __device__ __forceinline__ void wide_a_task(const ycx_nms_desc& d, const ycx_can
     const float X0 = o2f(s_ext[0]), Y0 = o2f(s_ext[1]);
     const float Ex = fmaxf(o2f(s_ext[2]) - X0, o2f(s_ext[3]) - Y0);
     const float inv = (Ex > 0.0f && Ex < INFINITY) ? 1.0f / Ex : 0.0f;
-    // (3) spatial counting sort on the fine grid (uniform trip count: the level ballots)
-    for (int rb = 0; rb < S; rb += 8 * kBigThreads) {  // batches of 8 ranks per thread
-      f32x4 bx[8];
+    // (3) spatial counting sort on the fine grid
+    {
+      LevelStats ls;
+      for (int rb = 0; rb < S; rb += 8 * kBigThreads) {  // batches of 8 ranks per thread
+        f32x4 bx[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int r = rb + j * kBigThreads + tid;
-        if (r < S) bx[j] = rbox[r];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-      const int r = rb + j * kBigThreads + tid;
-      if (rb + j * kBigThreads >= S) break;  // uniform: the level ballots need every lane
-      FGeo g;
-      g.level = -1;
-      if (r < S) {
-        g = fgeometry(bx[j], X0, Y0, inv, all_pairs);
-        atomicAdd(&cells[g.cell], 1u);
-      }
-      for (int Lv = 0; Lv < kFLevels; ++Lv) {
-        const bool in = r < S && g.level == Lv;
-        const unsigned long long m = __ballot(in);
-        if (!m) continue;
-        int mxw = in ? __float_as_int(g.w) : 0, mxh = in ? __float_as_int(g.h) : 0;
-        int mnw = in ? __float_as_int(g.w) : 0x7F800000, mnh = in ? __float_as_int(g.h) : 0x7F800000;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          mxw = max(mxw, __shfl_xor(mxw, o));
-          mxh = max(mxh, __shfl_xor(mxh, o));
-          mnw = min(mnw, __shfl_xor(mnw, o));
-          mnh = min(mnh, __shfl_xor(mnh, o));
+        for (int j = 0; j < 8; ++j) {
+          const int r = rb + j * kBigThreads + tid;
+          if (r < S) bx[j] = rbox[r];
         }
-        if (lane == 0) {
-          atomicAdd(&s_lv[Lv][0], __popcll(m));
-          atomicMax(&s_lv[Lv][1], mxw);
-          atomicMax(&s_lv[Lv][2], mxh);
-          atomicMin(&s_lv[Lv][3], mnw);
-          atomicMin(&s_lv[Lv][4], mnh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (rb + j * kBigThreads + tid < S) {
+            const FGeo g = fgeometry(bx[j], X0, Y0, inv, all_pairs);
+            atomicAdd(&cells[g.cell], 1u);
+            ls.add(g);
+          }
         }
       }
-      }
+      ls.flush(s_lv);
     }
     __syncthreads();
     {  // exclusive scan of the cell counts in place
@@ -1809,8 +1534,9 @@ __device__ __forceinline__ BigList big_list(const char* ws, const Layout& L, int
 
 // Suppressor search of positions [p0, p1) of one class (spatial order): every box's
 // higher-ranked boxes with IoU > thr, the highest-ranked kept in its 64-byte slot row
-// (kFast: 32 u16 ranks, the fast path's format; else 16 int ranks) and their count.
-template <bool kFast, class RankT>
+// (kSlot16: 32 u16 ranks, the fast path's format, for any class of S <= 65535; else 16 int
+// ranks) and their count. kFast: u16 cell ends (else u32).
+template <bool kFast, bool kSlot16, class RankT>
 __device__ __forceinline__ void search_range(const WFrame& f, const unsigned* cells, const int (*s_lv)[5],
                                              const f32x4* sbox, const RankT* srank, const Ptrs& P, int p0,
                                              int p1, const Thr& thr, float t_lo, float inv_t, int all_pairs) {
@@ -1829,7 +1555,7 @@ __device__ __forceinline__ void search_range(const WFrame& f, const unsigned* ce
     auto test = [&](int rj, const f32x4& o) {
       const bool cnd = rj < r && (all_pairs || (o[0] < b[2] && o[2] > b[0] && o[1] < b[3] && o[3] > b[1]));
       if (cnd && suppress(o[0], o[1], o[2], o[3], box_area(o), b[0], b[1], b[2], b[3], a, thr)) {
-        if constexpr (kFast) {
+        if constexpr (kSlot16) {
           unsigned short* s16 = reinterpret_cast<unsigned short*>(sl);
           if (ns < kFSlots) s16[ns] = (unsigned short)rj;
           else replace_slot16(s16, rj);
@@ -1842,21 +1568,30 @@ __device__ __forceinline__ void search_range(const WFrame& f, const unsigned* ce
     };
     f_ranges(cend, s_lv, g, S, t_lo, inv_t, [&](int q0, int q1) {
       int q = q0;
-      for (; q + 4 <= q1; q += 4) {
+      for (; q + 4 <= q1; q += 4) {  // four candidates in flight; a box is loaded only when it outranks
         int rj[4];
         f32x4 o[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          rj[u] = (int)srank[q + u];
-          o[u] = sbox[q + u];
-        }
+        for (int u = 0; u < 4; ++u) rj[u] = (int)srank[q + u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = rj[u] < r ? sbox[q + u] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int u = 0; u < 4; ++u) test(rj[u], o[u]);
       }
-      for (; q < q1; ++q) test((int)srank[q], sbox[q]);
+      for (; q < q1; ++q) {
+        const int rq = (int)srank[q];
+        if (rq < r) test(rq, sbox[q]);
+      }
     });
     P.nsup[off + p] = ns;
   }
+}
+
+// classes past u16 ranks (S > kSlot16Max)
+__device__ __forceinline__ void search_wide_int(const WFrame& f, const unsigned* cells, const int (*s_lv)[5],
+                                                          const Ptrs& P, int p0, int p1, const Thr& thr, float t_lo,
+                                                          float inv_t, int all_pairs) {
+  search_range<false, false>(f, cells, s_lv, P.sbox + f.off, P.srank + f.off, P, p0, p1, thr, t_lo, inv_t, all_pairs);
 }
 
 // Suppressor search of every split class: the concatenated positions of the list are cut into
@@ -1891,12 +1626,21 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
           lr[p] = (unsigned short)P.srank[f.off + p];
         }
         __syncthreads();
-        search_range<true>(f, cells, s_lv, lbox, lr, P, (int)(a - s0), (int)(b - s0), thr, t_lo, inv_t, all_pairs);
+        search_range<true, true>(f, cells, s_lv, lbox, lr, P, (int)(a - s0), (int)(b - s0), thr, t_lo, inv_t,
+                                 all_pairs);
       } else {
         const WFrame f = load_wide(ws, L, t, cells, s_lv);
         const Ptrs P = image_ptrs(ws, L, f.img);
-        search_range<false>(f, cells, s_lv, P.sbox + f.off, P.srank + f.off, P, (int)(a - s0), (int)(b - s0), thr,
-                            t_lo, inv_t, all_pairs);
+        constexpr int kCellB = ((kFCells * 4) + 15) & ~15;
+        if (S <= kSlot16Max) {  // the ranks (u16) staged beside the cells; boxes read from L2
+          unsigned short* lr = reinterpret_cast<unsigned short*>(smem + kCellB);
+          for (int p = threadIdx.x; p < S; p += kBigThreads) lr[p] = (unsigned short)P.srank[f.off + p];
+          __syncthreads();
+          search_range<false, true>(f, cells, s_lv, P.sbox + f.off, lr, P, (int)(a - s0), (int)(b - s0), thr, t_lo,
+                                    inv_t, all_pairs);
+        } else {
+          search_wide_int(f, cells, s_lv, P, (int)(a - s0), (int)(b - s0), thr, t_lo, inv_t, all_pairs);
+        }
       }
       __syncthreads();  // every read of this class's LDS done before the next one is staged
     }
@@ -1909,6 +1653,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
 // ever decides its rank), so a round touches only those, two at a time with their rank, count
 // and 64-byte slot row loaded together. Then the kept rows in rank order (each thread a
 // contiguous run of ranks, one scan).
+template <bool k16>
 __device__ __forceinline__ void resolve_wide(const Layout& L, char* ws, int t, const Task tk, char* smem,
                                                        int (*s_lv)[5], int* s_w, int* s_flag, const Thr thr,
                                                        float t_lo, float inv_t, int all_pairs) {
@@ -1940,20 +1685,28 @@ __device__ __forceinline__ void resolve_wide(const Layout& L, char* ws, int t, c
   }
   __syncthreads();
   YCX_WPROF_MARK(2)
+  // k16: 32 u16 slots per row (8 per 16-byte chunk); else 16 ints (4 per chunk)
+  constexpr int kCap = k16 ? kFSlots : kSlots, kPer = k16 ? 8 : 4;
   // res: 0 every suppressor removed (keep), 1 some undecided, 2 one kept (remove)
   auto decide = [&](int p, int r, int ns, const int4 (&s)[4]) -> int {
     int res = 0;
-    const int c = min(ns, kSlots);
+    const int c = min(ns, kCap);
 #pragma unroll
-    for (int h = 0; h < kSlots; ++h) {
-      const int4 x = s[h >> 2];
-      const int v = (h & 3) == 0 ? x.x : (h & 3) == 1 ? x.y : (h & 3) == 2 ? x.z : x.w;
-      if (h < c && res != 2) {
+    for (int h = 0; h < kCap; ++h) {
+      const int4 x = s[h / kPer];
+      int v;
+      if constexpr (k16) {
+        const int wv = ((h >> 1) & 3) == 0 ? x.x : ((h >> 1) & 3) == 1 ? x.y : ((h >> 1) & 3) == 2 ? x.z : x.w;
+        v = (int)(((unsigned)wv >> (16 * (h & 1))) & 0xFFFFu);
+      } else {
+        v = (h & 3) == 0 ? x.x : (h & 3) == 1 ? x.y : (h & 3) == 2 ? x.z : x.w;
+      }
+      if (h < c) {  // independent reads: no state read waits on the previous one
         const unsigned char sj = st[v];
-        res = sj == 1 ? 2 : (sj == 0 ? 1 : res);
+        res = max(res, sj == 1 ? 2 : (sj == 0 ? 1 : 0));
       }
     }
-    if (ns > kSlots && res == 0) {  // the cached ones are all removed: rescan
+    if (ns > kCap && res == 0) {  // the cached ones are all removed: rescan
       const f32x4 b = sbox[p];
       const float a = box_area(b);
       const FGeo g = fgeometry(b, f.X0, f.Y0, f.inv, all_pairs);
@@ -1993,10 +1746,12 @@ __device__ __forceinline__ void resolve_wide(const Layout& L, char* ws, int t, c
         const int ra = srank[pa], rb = srank[pb];
         const int na = nsup[pa], nb = nsup[pb];
         int4 sa[4], sb[4];
+        sa[0] = slots[(size_t)pa * 4];
+        sb[0] = slots[(size_t)pb * 4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          sa[q] = slots[(size_t)pa * 4 + q];
-          sb[q] = slots[(size_t)pb * 4 + q];
+        for (int q = 1; q < 4; ++q) {  // the further chunks only when they hold cached ranks
+          sa[q] = q * kPer < na ? slots[(size_t)pa * 4 + q] : int4{0, 0, 0, 0};
+          sb[q] = q * kPer < nb ? slots[(size_t)pb * 4 + q] : int4{0, 0, 0, 0};
         }
         const int resa = decide(pa, ra, na, sa);
         if (resa == 1) {
@@ -2113,11 +1868,7 @@ __device__ __forceinline__ void resolve_fast(const Layout& L, char* ws, int t, c
       int ns, res = 0;
       if (lds_csr) {
         ns = csr_ns[p];
-        const int b0 = csr_off[p], c = min(ns, kFSlots);
-        for (int j = 0; j < c && res != 2; ++j) {
-          const unsigned char sj = st[csr[b0 + j]];
-          res = sj == 1 ? 2 : (sj == 0 ? 1 : res);
-        }
+        res = csr_state(csr, (int)csr_off[p], min(ns, kFSlots), st);
       } else {
         ns = nsup[p];
         for_slots16(gsl + (size_t)p * (2 * kSlots), min(ns, kFSlots), [&](int, int v) {
@@ -2180,7 +1931,11 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   const Layout L = layout(d.n, d.rows_total);
   const BigList bl = big_list(ws, L, d.n);
   for (int t = blockIdx.x; t < bl.size(); t += gridDim.x) {
-    if (t < bl.nwide) resolve_wide(L, ws, t, bl.wide[t], smem, s_lv, s_w, &s_flag, thr, t_lo, inv_t, all_pairs);
+    if (t < bl.nwide) {
+      const Task tk = bl.wide[t];
+      if (tk.S <= kSlot16Max) resolve_wide<true>(L, ws, t, tk, smem, s_lv, s_w, &s_flag, thr, t_lo, inv_t, all_pairs);
+      else resolve_wide<false>(L, ws, t, tk, smem, s_lv, s_w, &s_flag, thr, t_lo, inv_t, all_pairs);
+    }
     else resolve_fast(L, ws, t - bl.nwide, smem, s_lv, s_w, &s_flag, thr, t_lo, inv_t, all_pairs);
   }
 }
@@ -2245,13 +2000,13 @@ Thr make_thr(double thr) {
 }  // namespace
 
 #ifdef YCX_NMS_PROFILE
-extern "C" int ycx_nms_prof_read(unsigned long long* out, int reset) {  // out[0..15] fast, [16..23] wide
+extern "C" int ycx_nms_prof_read(unsigned long long* out, int reset) {  // out[0..15] fast, [16..31] wide
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nms_prof), sizeof(g_nms_prof)) != hipSuccess) return 1;
-  if (hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_nms_wprof), sizeof(g_nms_wprof)) != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_nms_wprof), sizeof(g_nms_wprof)) != hipSuccess) return 1;  // out[16..31]
   if (reset) {
     unsigned long long z[16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_nms_prof), z, sizeof(z)) != hipSuccess) return 1;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_nms_wprof), z, 8 * sizeof(unsigned long long)) != hipSuccess) return 1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_nms_wprof), z, sizeof(z)) != hipSuccess) return 1;
   }
   return 0;
 }
