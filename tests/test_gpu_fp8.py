@@ -173,6 +173,54 @@ def test_fp8_conv_vs_dequantised_oracle(device, tile, case):
     assert near and frac >= 0.995, (frac, near)
 
 
+@pytest.mark.parametrize('tile', [34, 35])
+@pytest.mark.parametrize('n,hw,cin,cout,ex', [(2, (20, 20), 256, 128, 0), (3, (9, 13), 128, 128, 128),
+                                              (2, (10, 10), 512, 256, 0), (1, (7, 5), 128, 64, 0)])
+def test_fp8_conv_pool_fused(device, tile, n, hw, cin, cout, ex):
+    """MP fused into the fp8 1x1 conv (ycx_conv_desc.in_pool: the k2 s2 max-pool of the (2h, 2w)
+    e4m3 map formed in the operand staging, tiles 34 / 35) vs ycx_maxpool (fp8) then the same
+    tile on the pooled map: bit for bit. Ragged pixel tails, channel-sliced input, negative
+    and zero activations in the windows."""
+    from ycx.engine import pack_fp8_weights
+    cpad = -(-cout // 64) * 64
+    if tile == 34 and cpad % 128:
+        pytest.skip("tile 34 is 128 output channels wide")
+    g = torch.Generator().manual_seed(17)
+    h, w = hw
+    x = torch.randn(n, 2 * h, 2 * w, cin + ex, generator=g)
+    x[x.abs() < 0.05] = 0.0
+    xq = _q(x, 16.0)
+    wt = torch.randn(cpad, cin, 1, 1, generator=g, dtype=torch.float64) / cin ** 0.5
+    wt[cout:] = 0
+    wq, sw = pack_fp8_weights(wt)
+    bias = torch.cat([torch.randn(cpad, generator=g, dtype=torch.float64) * 0.1, 1.0 / (sw * 16.0)]).float()
+    xd, wd, bd = xq.view(torch.uint8).to(device), wq.view(torch.uint8).to(device), bias.to(device)
+    pooled = torch.zeros(n, h, w, cin, dtype=torch.uint8, device=device)
+    pd = L.PoolDesc()
+    pd.n, pd.h, pd.w, pd.c, pd.in_c_off, pd.in_c_stride = n, 2 * h, 2 * w, cin, ex, cin + ex
+    pd.ho, pd.wo, pd.out_c_off, pd.out_c_stride, pd.k, pd.stride, pd.pad, pd.dtype = h, w, 0, cin, 2, 2, 0, L.DT_FP8
+    pd.levels = 1
+    L.check(L.lib.ycx_maxpool(ctypes.byref(pd), xd.data_ptr(), pooled.data_ptr(), L.stream_handle(device)))
+
+    def conv(src, in_off, in_stride, in_pool):
+        y = torch.zeros(n, h, w, cout + 8, dtype=torch.uint8, device=device)
+        d = L.ConvDesc()
+        d.n, d.h, d.w, d.cin, d.in_c_off, d.in_c_stride = n, h, w, cin, in_off, in_stride
+        d.ho, d.wo, d.cout, d.cout_pad, d.out_c_off, d.out_c_stride = h, w, cout, cpad, 8, cout + 8
+        d.kh = d.kw = d.stride = 1
+        d.pad, d.act, d.dtype, d.out_layout, d.tile, d.in_pool = 0, L.ACT_SILU, L.DT_FP8, L.OUT_NHWC, tile, in_pool
+        d.out_scale = 32.0
+        L.check(L.lib.ycx_conv2d(ctypes.byref(d), src.data_ptr(), wd.data_ptr(), bd.data_ptr(), y.data_ptr(), None,
+                                 L.stream_handle(device)), "fp8 conv")
+        return y
+
+    fused = conv(xd, ex, cin + ex, 1)
+    ref = conv(pooled, 0, cin, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(fused.cpu(), ref.cpu())
+    assert torch.all(fused[..., :8] == 0)
+
+
 def test_fp8_tile_choice_and_rejects(device):
     d = L.ConvDesc()
     d.n, d.h, d.w, d.cin, d.in_c_off, d.in_c_stride = 32, 80, 80, 256, 0, 256
@@ -206,7 +254,8 @@ def test_yolov7_640_fp8_vs_oracle(device, v7_fp8):
     assert max(errs) < FP8_TOL, errs
     eng = m.engine_for(x.shape, device)
     assert eng.dt == L.DT_FP8 and all(t.dtype == torch.float8_e4m3fn for t in eng.buffers)
-    names = {i['name'] for i in eng.op_info if i['kind'] == 'conv'}
+    names = {i['name'].split('+')[0] for i in eng.op_info if i['kind'] == 'conv'}  # '+maxpool_k2s2': MP fused
+    assert sum(1 for i in eng.op_info if i['name'].endswith('+maxpool_k2s2')) == 5
     assert names <= {'f8_co128_px128_k128_s2', 'f8_co64_px128_k128_s2', 'f8_wres1x1', 'f8_halo3x3_ws_co64'}, names
     # every scale is a power of two and the calibrated maxima sit in [224, 448)
     assert all(float(s).hex().startswith(('0x1.0000000000000p', '0x1p')) for s in eng.scales.values())

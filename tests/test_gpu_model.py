@@ -183,16 +183,18 @@ def test_conv_pair_fusion_bit_identical(device, monkeypatch):
             assert torch.equal(a, b)
 
 
-def test_pool_fusion_bit_identical(device):
-    """yolov7 bf16 plan with the MP pools fused into their 1x1 convs == the plan that runs
-    them as ycx_maxpool ops, bit for bit."""
+@pytest.mark.parametrize('prec', ['bf16', 'fp8'])
+def test_pool_fusion_bit_identical(device, prec):
+    """yolov7 bf16 / fp8 plan with the MP pools fused into their 1x1 convs == the plan that
+    runs them as ycx_maxpool ops, bit for bit."""
     from ycx.engine import Engine
-    m, _ = make_model('yolov7', 80, 0, 'bf16')
+    m, _ = make_model('yolov7', 80, 0, prec)
     m.to(device)
     x = synthetic_images(2, 3, 320, 320, seed=4).to(device)
+    amax = m.calibrate_fp8(device=device, hw=(320, 320), n=2) if prec == 'fp8' else None
     outs = []
     for fuse in (True, False):
-        eng = Engine(m, tuple(x.shape), torch.device(device), 'bf16', fuse_pool=fuse)
+        eng = Engine(m, tuple(x.shape), torch.device(device), prec, fuse_pool=fuse, fp8_amax=amax)
         try:
             assert sum(1 for i in eng.op_info if i['name'].endswith('+maxpool_k2s2')) == (5 if fuse else 0)
             outs.append([o.clone() for o in eng.run(x)])

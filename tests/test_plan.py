@@ -53,8 +53,8 @@ def test_plan_yolov7_layout():
 
 def test_pool_fusion_pass_finds_the_mp_blocks():
     """The engine's MP-pool fusion pass (host logic, no GPU): every yolov7 k2 s2 pool feeds
-    exactly one 1x1 / s1 conv and is fused into it; in yolov7-tiny only pools read by a lone 1x1
-    fuse; fp8 / f32 plans and fuse_pool=False keep every pool."""
+    exactly one 1x1 / s1 conv and is fused into it (bf16, and fp8 where cin % 128 == 0: all five);
+    in yolov7-tiny only pools read by a lone 1x1 fuse; f32 plans and fuse_pool=False keep every pool."""
     from ycx import _lib as L
     from ycx.engine import Engine
 
@@ -71,7 +71,9 @@ def test_pool_fusion_pass_finds_the_mp_blocks():
         assert (p['k'], p['s'], p['p']) == (2, 2, 0) and pool.inputs[0].h == 2 * pool.out.h
         (conv,) = pool.out.consumers
         assert conv.kind == 'conv' and (conv.p['k'], conv.p['s'], conv.p['p']) == (1, 1, 0)
-    assert pairs('yolov7', 80, dt=L.DT_FP8) == {} and pairs('yolov7', 80, dt=L.DT_F32) == {}
+    f8 = pairs('yolov7', 80, dt=L.DT_FP8)
+    assert len(f8) == 5 and all(int(pool.out.consumers[0].p['w'].shape[1]) % 128 == 0 for pool in f8.values())
+    assert pairs('yolov7', 80, dt=L.DT_F32) == {}
     assert pairs('yolov7', 80, fuse=False) == {}
     for pool in pairs('yolov7-tiny', 1).values():
         assert pool.out.consumers[0].p['k'] == 1

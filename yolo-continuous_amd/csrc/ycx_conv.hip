@@ -1193,11 +1193,17 @@ __device__ __forceinline__ void epilogue_f8(const ConvArgs& a, const f32x4 (&acc
   }
 }
 
-template <int BM, int BN, int WM, int WN, int TPS, bool HEAD = false>
-__global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a, HeadArgs hd) {
+// POOL (1x1 / s1 / p0, cin % 128 == 0): the activation operand is MP's k2 s2 max-pool of the
+// (2H, 2W) map x, formed while staging as in conv_bf16_glds: step t issues the weight DMA of
+// t + 1 and four 16-byte loads per pixel row (the 2x2 window, 16 channels per lane), and after
+// step t's MFMAs takes the max in fp32 in ycx_maxpool's window order and writes the re-encoded
+// bytes (exact: the max is one of the inputs) where the activation DMA would have put them.
+template <int BM, int BN, int WM, int WN, int TPS, bool HEAD = false, bool POOL = false>
+__global__ void __launch_bounds__(WM * WN * 64, POOL ? 4 : 1) conv_f8_glds(ConvArgs a, HeadArgs hd) {  // POOL: 2 blocks / CU
   constexpr int NW = WM * WN, NST = 2;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(TPS == 0 || TPS == 1 || TPS == 2 || TPS == 4, "taps per K step (0: any cin % 16 == 0)");
+  static_assert(!POOL || (TPS == 1 && !HEAD), "pooled operand: one tap of 128 channels per K step");
   constexpr int RB = 128;                   // bytes per operand row per K step
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -1245,17 +1251,64 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a, HeadArg
     const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
     b_iy0[i] = ok ? oy * a.S - a.P : -(1 << 20);  // tail rows fail the bounds test
     b_ix0[i] = ox * a.S - a.P;
-    b_base[i] = ((n * a.H + b_iy0[i]) * a.W + b_ix0[i]) * a.in_cs + a.in_coff + cbyte;
+    if constexpr (POOL)  // byte offset of the window's top-left pixel; -1: tail row (zeros)
+      b_base[i] = ok ? ((n * 2 * a.H + 2 * oy) * 2 * a.W + 2 * ox) * a.in_cs + a.in_coff + cbyte : -1;
+    else
+      b_base[i] = ((n * a.H + b_iy0[i]) * a.W + b_ix0[i]) * a.in_cs + a.in_coff + cbyte;
   }
   // this lane's tap for the next stage to issue (TPS > 1), or the block-wide
   // (tap, channel block) position (TPS == 1)
   const int ntaps = a.KH * a.KW;
   int l_tap = tsel, ky = tsel / a.KW, kx = tsel - (tsel / a.KW) * a.KW;
   int cb = TPS == 0 ? 16 * lch - tsel * a.Cin : 0;
-  auto issue = [&](int s, int buf) {
+  auto issueA = [&](int s, int buf) {
     char* base = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * RB, base + (wid + NW * i) * 1024);
+  };
+  // POOL: the window's four 16-byte rows of the next K step in flight in registers, pooled
+  // into LDS after the MFMAs (no VALU on them before, which would wait for the loads)
+  int4 pw[POOL ? B_PW : 1][4];
+  int pcb = 0;  // channel byte of the next pooled K step
+  auto loadB = [&]() {
+    const int cs = a.in_cs, rs = 2 * a.W * a.in_cs;
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      const uint8_t* src = X + (b_base[i] < 0 ? 0 : b_base[i] + pcb);
+      pw[i][0] = *reinterpret_cast<const int4*>(src);
+      pw[i][1] = *reinterpret_cast<const int4*>(src + cs);
+      pw[i][2] = *reinterpret_cast<const int4*>(src + rs);
+      pw[i][3] = *reinterpret_cast<const int4*>(src + rs + cs);
+    }
+    pcb += RB;
+  };
+  auto writeB = [&](int buf) {
+    char* base = smem + buf * STAGE + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      int o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int w0 = q == 0 ? pw[i][0].x : q == 1 ? pw[i][0].y : q == 2 ? pw[i][0].z : pw[i][0].w;
+        const int w1 = q == 0 ? pw[i][1].x : q == 1 ? pw[i][1].y : q == 2 ? pw[i][1].z : pw[i][1].w;
+        const int w2 = q == 0 ? pw[i][2].x : q == 1 ? pw[i][2].y : q == 2 ? pw[i][2].z : pw[i][2].w;
+        const int w3 = q == 0 ? pw[i][3].x : q == 1 ? pw[i][3].y : q == 2 ? pw[i][3].z : pw[i][3].w;
+        // ycx_maxpool's order: (0,0), (0,1), (1,0), (1,1), from -inf
+#define YCX_F8_MAX4(J)                                                                     \
+  fmaxf(fmaxf(fmaxf(fmaxf(-INFINITY, __builtin_amdgcn_cvt_f32_fp8(w0, J)),               \
+                    __builtin_amdgcn_cvt_f32_fp8(w1, J)), __builtin_amdgcn_cvt_f32_fp8(w2, J)), \
+        __builtin_amdgcn_cvt_f32_fp8(w3, J))
+        o[q] = b_base[i] < 0 ? 0 : (int)f8x4_pack(YCX_F8_MAX4(0), YCX_F8_MAX4(1), YCX_F8_MAX4(2), YCX_F8_MAX4(3));
+#undef YCX_F8_MAX4
+      }
+      *reinterpret_cast<int4*>(base + (wid + NW * i) * 1024 + lane * 16) = int4{o[0], o[1], o[2], o[3]};
+    }
+    // the next raw s_barrier does not wait for LDS stores by itself: complete them here
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto issue = [&](int s, int buf) {
+    issueA(s, buf);
+    char* base = smem + buf * STAGE;
     const bool tap_ok = TPS == 1 || l_tap < ntaps;
     const int tap = (ky * a.W + kx) * a.in_cs + cb;
 #pragma unroll
@@ -1292,12 +1345,25 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a, HeadArg
 
   const int nt = a.nsteps;
   const int c0 = 2 * (lane >> 4);
-  issue(0, 0);
+  if constexpr (POOL) {
+    issueA(0, 0);
+    loadB();
+    writeB(0);
+  } else {
+    issue(0, 0);
+  }
   for (int t = 0; t < nt; ++t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < nt) issue(t + 1, (t + 1) & 1);
+    if constexpr (POOL) {
+      if (t + 1 < nt) {
+        issueA(t + 1, (t + 1) & 1);
+        loadB();
+      }
+    } else {
+      if (t + 1 < nt) issue(t + 1, (t + 1) & 1);
+    }
     const char* A = smem + (t & 1) * STAGE;
     const char* B = A + A_BYTES;
     i32x8 af[FM], bfr[FN];
@@ -1322,6 +1388,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_f8_glds(ConvArgs a, HeadArg
       for (int j = 0; j < FN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
     __builtin_amdgcn_sched_barrier(0);
+    // slot (t + 1) & 1 held step t - 1, which every wave finished before this step's barrier
+    if constexpr (POOL)
+      if (t + 1 < nt) writeB((t + 1) & 1);
   }
   static_assert(FM % 2 == 0, "fragment pairs");
   if constexpr (HEAD) {
@@ -3401,6 +3470,11 @@ ycx_status launch_f8(ConvArgs a, hipStream_t st) {
   a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
   a.gc = glds_gc(a);
   const dim3 g(a.nwg), b(WM * WN * 64);
+  if (a.pool) {  // fused MP (ycx_conv_desc.in_pool): one 128-channel tap per K step
+    if (tps != 1) return YCX_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 1, false, true>), g, b, 0, st, a, HeadArgs{});
+    return ycx_launch_status();
+  }
   if (tps == 4) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 4>), g, b, 0, st, a, HeadArgs{});
   else if (tps == 2) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 2>), g, b, 0, st, a, HeadArgs{});
   else if (tps == 1) hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 1>), g, b, 0, st, a, HeadArgs{});
@@ -3551,8 +3625,11 @@ extern "C" const char* ycx_conv_tile_name(int32_t tile) {
 static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wres: no residual (tiles 22, 23)
   if (d->dtype == YCX_DT_F32) return 8;
   const long long M = (long long)d->n * d->ho * d->wo;
-  if (d->in_pool)  // the pooled-operand variants of the two-stage LDS-DMA tiles
-    return d->cout_pad % 128 == 0 && (d->cout_pad / 128) * ((M + 127) / 128) >= 256 ? 16 : 18;
+  if (d->in_pool) {  // the pooled-operand variants of the two-stage LDS-DMA tiles
+    const bool big = d->cout_pad % 128 == 0 && (d->cout_pad / 128) * ((M + 127) / 128) >= 256;
+    if (d->dtype == YCX_DT_FP8) return big ? 34 : 35;
+    return big ? 16 : 18;
+  }
   if (d->dtype == YCX_DT_FP8) {
     // pointwise layers with cin in {128, 256, 512} and >= 8 pixel tiles per persistent block:
     // weights resident in registers (tile 36)
@@ -3690,17 +3767,19 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x,
   // The 32-bit index math inside the kernels.
   YCX_CHECK_SUPPORTED((long long)d->n * d->ho * d->wo < (1LL << 31));
   YCX_CHECK_SUPPORTED((long long)d->cout_pad * d->kh * d->kw * d->cin < (1LL << 31));
-  if (d->in_pool) {  // fused MP: bf16 pointwise over a (2h, 2w) map
+  if (d->in_pool) {  // fused MP: 16-bit or fp8 (cin % 128 == 0) pointwise over a (2h, 2w) map
     YCX_CHECK_ARG(d->in_pool == 1);
-    YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_ELT && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0);
-    YCX_CHECK_SUPPORTED((long long)d->n * 4 * d->h * d->w * d->in_c_stride * 2 < (1LL << 31));
+    YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_ELT || (d->dtype == YCX_DT_FP8 && d->cin % 128 == 0)) && d->kh == 1 &&
+                        d->kw == 1 && d->stride == 1 && d->pad == 0);
+    YCX_CHECK_SUPPORTED((long long)d->n * 4 * d->h * d->w * d->in_c_stride * (d->dtype == YCX_DT_FP8 ? 1 : 2) <
+                        (1LL << 31) - 64);
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ConvArgs a = make_args(d, x, w, bias, y, residual);
 
   int tile = d->tile ? d->tile : pick_tile(d, residual == nullptr);  // tile 22 stores no residual
   YCX_CHECK_SUPPORTED(tile > 0 && tile < kNumTiles);
-  YCX_CHECK_SUPPORTED(!d->in_pool || tile == 16 || tile == 18 || tile == 25);
+  YCX_CHECK_SUPPORTED(!d->in_pool || tile == 16 || tile == 18 || tile == 25 || tile == 34 || tile == 35);
   const TileInfo& t = kTiles[tile];
   YCX_CHECK_SUPPORTED(d->cin % t.bk == 0 && d->cout_pad % t.bm == 0);
   YCX_CHECK_SUPPORTED((d->dtype == YCX_DT_FP8) == (tile >= 34 && tile <= 37));

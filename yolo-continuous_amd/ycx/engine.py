@@ -849,10 +849,11 @@ class Engine:
 
     def _pool_convs(self):
         """MP's k2 s2 pools (nets/common.py:25-31) whose map is read only by one 1x1 / s1
-        conv: the conv pools its operand while staging it (ycx_conv_desc.in_pool, bf16
-        plans), so the pooled map is never written. yolov7: all five MP pools.
-        Returns {id(conv node): pool node}."""
-        if not self.h16 or not self.fuse_pool or os.environ.get('YCX_NO_POOL_FUSE'):
+        conv: the conv pools its operand while staging it (ycx_conv_desc.in_pool, 16-bit
+        plans, and fp8 plans where cin % 128 == 0), so the pooled map is never written.
+        yolov7: all five MP pools. Returns {id(conv node): pool node}."""
+        fp8 = self.dt == L.DT_FP8
+        if not (self.h16 or fp8) or not self.fuse_pool or os.environ.get('YCX_NO_POOL_FUSE'):
             return {}
         out = {}
         for nd in self.graph.nodes:
@@ -868,9 +869,9 @@ class Engine:
             if c.kind != 'conv' or c.inputs[0] is not v or not (q['k'] == 1 and q['s'] == 1 and q['p'] == 0):
                 continue
             cin, cout = int(q['w'].shape[1]), int(q['w'].shape[0])
-            if cin % 64 or self._cout_pad(cout) % 64 or q['layout'] == L.OUT_NCHW_F32:
+            if cin % (128 if fp8 else 64) or self._cout_pad(cout) % 64 or q['layout'] == L.OUT_NCHW_F32:
                 continue
-            if x.n * x.h * x.w * x.buf.c * 2 >= 1 << 31:
+            if x.n * x.h * x.w * x.buf.c * (1 if fp8 else 2) >= (1 << 31) - 64:
                 continue
             out[id(c)] = nd
         return out
