@@ -93,7 +93,8 @@ typedef struct ycx_conv_desc {
   float res_scale;          /* YCX_DT_FP8 only: residual dequantisation (1 / s_res) */
   int32_t in_pool;          /* 1: x is the (2h, 2w) map that MP's k2 s2 max-pool reduces to the
                              * (h, w) input (nets/common.py:25-31), pooled in the conv's operand
-                             * staging (bf16 1x1/s1/p0, cin % 64 == 0); 0: x is the input */
+                             * staging (1x1/s1/p0: 16-bit with cin % 64 == 0, or YCX_DT_FP8
+                             * with cin % 128 == 0, r04); 0: x is the input */
 } ycx_conv_desc;
 
 /* Max-pool, NHWC, pad value -inf (torch.nn.MaxPool2d semantics, floor mode).
