@@ -11,3 +11,8 @@ for i in 1 2; do for lib in $AB_A $AB_B; do for c in ${AB_CONFIGS:-c2 c4}; do
   python -c "
 import json; d=json.loads(open('$O/ab2_$c.log').read().strip().splitlines()[-1]); print('$c', '$lib', d['value'], d['p50_ms'], d['p50_ms_unloaded'])"
 done; done; done
+if [ -n "$AB_MICRO" ]; then for lib in $AB_A $AB_B; do for sh in -3 0; do
+  YCX_LIB=$L/libycx_$lib.so timeout -k 10 300 python bench.py --post-micro --obj-shift $sh > $O/ab2_micro.log 2>&1 || exit 1
+  python -c "
+import json; d=json.loads(open('$O/ab2_micro.log').read().strip().splitlines()[-1]); print('micro shift $sh', '$lib', d['value'], d.get('ms_per_step'))"
+done; done; fi

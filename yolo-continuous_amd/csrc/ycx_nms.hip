@@ -205,14 +205,6 @@ __device__ __forceinline__ float bcast(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
-template <int R>
-__device__ __forceinline__ float pick(const float (&a)[R], int r) {
-  float v = a[0];
-#pragma unroll
-  for (int k = 1; k < R; ++k) v = (r == k) ? a[k] : v;
-  return v;
-}
-
 // A whole class in registers: position e = r*64 + lane, r < R.
 template <int R>
 __device__ void class_in_registers(const ycx_cand* __restrict__ ci, const int* __restrict__ bucket,
@@ -267,20 +259,27 @@ __device__ void class_in_registers(const ycx_cand* __restrict__ ci, const int* _
     }
   }
   unsigned rm = 0u, km = 0u;  // bit r: position r*64+lane removed / kept
-  for (int i = 0; i < S; ++i) {
-    const int ri = i >> 6, li = i & 63;
-    if ((__builtin_amdgcn_readlane(rm, li) >> ri) & 1u) continue;
-    if (lane == li) km |= 1u << ri;
-    const float bx1 = bcast(pick<R>(x1, ri), li), by1 = bcast(pick<R>(y1, ri), li);
-    const float bx2 = bcast(pick<R>(x2, ri), li), by2 = bcast(pick<R>(y2, ri), li);
-    const float ba = bcast(pick<R>(ar, ri), li);
+  // greedy scan in rank order i = ri * 64 + li; the slot ri is a compile-time constant of the
+  // unrolled outer loop, so box i's registers are read by index, never through a dynamically
+  // indexed array (a select chain over the slots was folded into one, which lives in scratch)
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (r < ri) continue;  // uniform: every position of an earlier slot precedes i
-      const int e = r * 64 + lane;
-      if (e > i && e < S && !((rm >> r) & 1u) &&
-          suppress(bx1, by1, bx2, by2, ba, x1[r], y1[r], x2[r], y2[r], ar[r], thr))
-        rm |= 1u << r;
+  for (int ri = 0; ri < R; ++ri) {
+    if (ri * 64 >= S) break;  // uniform
+    const int lim = min(64, S - ri * 64);
+    for (int li = 0; li < lim; ++li) {
+      const int i = ri * 64 + li;
+      if ((__builtin_amdgcn_readlane(rm, li) >> ri) & 1u) continue;
+      if (lane == li) km |= 1u << ri;
+      const float bx1 = bcast(x1[ri], li), by1 = bcast(y1[ri], li);
+      const float bx2 = bcast(x2[ri], li), by2 = bcast(y2[ri], li);
+      const float ba = bcast(ar[ri], li);
+#pragma unroll
+      for (int r = ri; r < R; ++r) {  // every position of an earlier slot precedes i
+        const int e = r * 64 + lane;
+        if (e > i && e < S && !((rm >> r) & 1u) &&
+            suppress(bx1, by1, bx2, by2, ba, x1[r], y1[r], x2[r], y2[r], ar[r], thr))
+          rm |= 1u << r;
+      }
     }
   }
   int base = 0;  // kept rows, compacted in sorted (score-descending) order
