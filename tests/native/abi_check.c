@@ -116,8 +116,13 @@ int main(void) {
   EXPECT(ycx_debug_bounds(oob, 0) == YCX_ERR_UNSUPPORTED && oob[0] == 0); /* release build */
   EXPECT(ycx_debug_bounds(NULL, 0) == YCX_ERR_BAD_ARG);
   EXPECT(ycx_set_trace(0) == YCX_OK);
-  EXPECT(ycx_set_trace(1) == YCX_OK); /* roctx resolved at run time (dlopen), not at link time */
-  EXPECT(ycx_set_trace(0) == YCX_OK);
+  {
+    /* roctx is resolved at run time (dlopen), not at link time: a build host without the
+       profiler SDK gets YCX_ERR_UNSUPPORTED and tracing stays off */
+    ycx_status st = ycx_set_trace(1);
+    EXPECT(st == YCX_OK || st == YCX_ERR_UNSUPPORTED);
+    EXPECT(ycx_set_trace(0) == YCX_OK);
+  }
 
   if (fails) {
     fprintf(stderr, "abi_check: %d failures\n", fails);

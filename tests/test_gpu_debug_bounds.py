@@ -16,7 +16,7 @@ DBG = os.path.join(REPO, "yolo-continuous_amd", "ycx", "libycx_hip_dbg.so")
 
 def test_no_out_of_bounds_stores():
     if not os.path.exists(DBG):
-        pytest.skip("libycx_hip_dbg.so not built (YCX_BUILD_DEBUG=0): make -C yolo-continuous_amd/csrc debug")
+        pytest.skip("libycx_hip_dbg.so not built (opt-in: YCX_BUILD_DEBUG=1 build()): make -C yolo-continuous_amd/csrc debug")
     env = dict(os.environ, YCX_LIB=DBG)
     r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "probes", "bounds_run.py")], env=env,
                        capture_output=True, text=True, timeout=600)

@@ -59,17 +59,28 @@ def test_nms_keep_rows_bit_exact(device, manifest, g3, name):
         assert (keep[b, k:] == -1).all()
 
 
+def misaligned(h):
+    """The same values at a 4-byte (not 16-byte) aligned address: ycx_decode_filter then
+    takes its one-row-per-thread kernel (decode_filter_kernel), as it does for heads with
+    h*w % 4 != 0 or unaligned pointers."""
+    buf = torch.empty(h.numel() + 4, dtype=h.dtype, device=h.device)
+    v = buf[1:1 + h.numel()].view(h.shape)
+    v.copy_(h)
+    assert v.data_ptr() % 16 != 0 and v.is_contiguous()
+    return v
+
+
 @pytest.mark.parametrize('scalar', [False, True])
 @pytest.mark.parametrize('name', CASES)
-def test_device_post_g3(device, manifest, g3, name, scalar, monkeypatch):
+def test_device_post_g3(device, manifest, g3, name, scalar):
     """DevicePost (fused ycx_decode_filter + ycx_sort_nms, the Detector's post and
     bench.py --post-micro) on the G3 head logits vs the golden keep rows. The
     fused filter evaluates the sigmoids on the GPU, so a candidate at the conf
     boundary may flip by an ulp; no systematic difference is allowed."""
-    if scalar:  # the one-row-per-thread kernel (heads with h*w % 4 != 0 or unaligned take it)
-        monkeypatch.setenv('YCX_DECODE_SCALAR', '1')
     e = manifest['g3'][name]
     heads = [h.to(device).contiguous() for h in g3_heads(e)]
+    if scalar:  # the one-row-per-thread kernel (heads with h*w % 4 != 0 or unaligned take it)
+        heads = [misaligned(h) for h in heads]
     post = DevicePost(heads, e['nc'], ANCHORS, MASK, (e['size'], e['size']), device, e['conf'], e['iou'],
                       max_det=8192)  # nc3_dense keeps ~1.9k rows per image
     dets, keep, kc = post()
@@ -90,13 +101,11 @@ def test_device_post_g3(device, manifest, g3, name, scalar, monkeypatch):
 
 
 @pytest.mark.parametrize('scalar', [False, True])
-def test_device_post_sparse_class_ties(device, scalar, monkeypatch):
+def test_device_post_sparse_class_ties(device, scalar):
     """Sparse rows through both decode_filter kernels (four rows per thread; one
     row per thread with the wave-cooperative class scan for <= 8 rows per wave): ties resolve to the first class (torch.max,
     detect.py:108), a maximum past class 63 is found, and the kept rows and
     classes equal the oracle's."""
-    if scalar:
-        monkeypatch.setenv('YCX_DECODE_SCALAR', '1')
     nc, bs, size = 80, 2, 640
     g = torch.Generator().manual_seed(5)
     shapes = [(size // k, size // k) for k in (32, 16, 8)]
@@ -120,7 +129,8 @@ def test_device_post_sparse_class_ties(device, scalar, monkeypatch):
                     hd[b, a, 5:, y, x] = -1.0
                     hd[b, a, 5 + 79, y, x] = 3.0             # past the first 64 lanes
     heads = [hd.reshape(bs, 3 * (5 + nc), h, w).contiguous() for hd, (h, w) in zip(heads, shapes)]
-    post = DevicePost([h.to(device) for h in heads], nc, ANCHORS, MASK, (size, size), device, 0.3, 0.45, 1000)
+    post = DevicePost([misaligned(h.to(device)) if scalar else h.to(device) for h in heads], nc, ANCHORS, MASK,
+                      (size, size), device, 0.3, 0.45, 1000)
     dets, keep, kc = post()
     torch.cuda.synchronize()
     dec = torch.cat(ref_post.decode_box(heads, A, MASK, nc, (size, size)), 1)
@@ -147,15 +157,13 @@ def test_sigmoid_monotone_every_float(device):
 
 
 @pytest.mark.parametrize('scalar', [True, False])
-def test_device_post_dense_class_scan(device, scalar, monkeypatch):
+def test_device_post_dense_class_scan(device, scalar):
     """Dense waves (every row passes on objectness) with crafted class logits:
     saturated ties (several logits past ~17 give sigmoid 1.0: first such class),
     exact ties, near-ties one float apart, +inf, -inf and NaN (class 0 NaN sticks,
     later NaNs never win). Every candidate's (cls, cls_conf) equals the
     sequential strict-'>' scan over the device's own sigmoids (ycx_decode),
     i.e. the exact class argmax is the scan bit for bit."""
-    if scalar:
-        monkeypatch.setenv('YCX_DECODE_SCALAR', '1')
     nc, bs, size = 80, 2, 320
     g = torch.Generator().manual_seed(11)
     shapes = [(size // k, size // k) for k in (32, 16, 8)]
@@ -195,7 +203,7 @@ def test_device_post_dense_class_scan(device, scalar, monkeypatch):
                 flat[r, 5 + j + 1:] = -250.0
         hd.copy_(flat.reshape(hd.shape[0], hd.shape[1], hd.shape[3], hd.shape[4], 5 + nc).permute(0, 1, 4, 2, 3))
     heads = [hd.reshape(bs, 3 * (5 + nc), h, w).contiguous() for hd, (h, w) in zip(heads, shapes)]
-    dh = [h.to(device) for h in heads]
+    dh = [misaligned(h.to(device)) if scalar else h.to(device) for h in heads]
     post = DevicePost(dh, nc, ANCHORS, MASK, (size, size), device, 0.0, 0.45, 100)
     post.counts.zero_()
     post()

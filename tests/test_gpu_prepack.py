@@ -40,3 +40,23 @@ def test_prepack_rejects_other_plan(device, tmp_path):
     other.to(device)
     with pytest.raises(ValueError, match='do not match this plan'):
         other(torch.zeros(1, 3, 320, 320, device=device))
+
+
+@pytest.mark.parametrize('precision', ['fp16', 'bf16'])
+def test_prepack_yolov7_pair_batch_independent(device, tmp_path, precision):
+    """the 1x1 pair (tile 55) forms only at bs >= 6 on a 640^2 yolov7, and
+    prepack.save packs at bs 1. Tensors are named by conv node, so a file written at bs 1
+    binds the right weights to both convs of the pair at bs 6: bit-identical outputs."""
+    src, _ = make_model('yolov7', 80, 0, precision)
+    src.to(device)
+    x = synthetic_images(6, 3, 640, 640, seed=5).to(device)
+    ref = [o.clone() for o in src(x)]
+    assert any(i['kind'] == 'conv_pair' for i in src.engine_for(x.shape, device, slot=src.EAGER_SLOT).op_info)
+    path = str(tmp_path / f"v7_{precision}.safetensors")
+    src.save_prepacked(path, (640, 640))
+    dst, _ = make_model('yolov7', 80, 7, 'bf16')
+    dst.load_prepacked(path)
+    dst.to(device)
+    out = dst(x)
+    for a, b in zip(out, ref):
+        assert torch.equal(a, b)

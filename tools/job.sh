@@ -1,15 +1,15 @@
 #!/bin/bash
-# Round-4 GPU jobs (run through gpurun):  bash tools/r04.sh JOB [args]
+# GPU jobs (run through gpurun):  YCX_ROUND=r05 bash tools/job.sh JOB [args]
 # Every GPU step has its own time limit and the steps are chained with &&.
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R" || exit 1
-O=$R/gpurun_out/r04
+O=$R/gpurun_out/${YCX_ROUND:-r05}
 mkdir -p "$O"
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
 job=$1
 shift
 case "$job" in
-  tests)  # a test selection: bash tools/r04.sh tests 'tests/test_x.py::y' ...
+  tests)  # a test selection: bash tools/job.sh tests 'tests/test_x.py::y' ...
     timeout -k 10 900 $PYT -s "$@" > "$O/tests.log" 2>&1; rc=$?
     tail -30 "$O/tests.log"; exit $rc ;;
   bench)  # the default bench + the per-op gap table
@@ -24,7 +24,7 @@ case "$job" in
     YCX_BENCH_KERNELS=$O/ops.json timeout -k 10 400 python bench.py > "$O/bench.log" 2>&1 || { tail -20 "$O/bench.log"; exit 1; }
     tail -1 "$O/bench.log" | cut -c1-1500
     python tools/op_gap.py "$O/ops.json" > "$O/op_gap.md" ;;
-  probe)  # a probe script: bash tools/r04.sh probe tests/probes/x.py args
+  probe)  # a probe script: bash tools/job.sh probe tests/probes/x.py args
     timeout -k 10 600 python -u "$@" > "$O/probe.log" 2>&1; rc=$?
     tail -60 "$O/probe.log"; exit $rc ;;
   *) echo "unknown job $job"; exit 2 ;;

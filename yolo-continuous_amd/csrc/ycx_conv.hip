@@ -1431,261 +1431,6 @@ __global__ void __launch_bounds__(WM * WN * 64, POOL ? 4 : 1) conv_f8_glds(ConvA
   }
 }
 
-#ifdef YCX_EXPERIMENTAL_TILES  // retired: measured 0.5-0.9x of the picked tiles
-// -------------------------------------------------------------------------
-// bf16 implicit-GEMM conv, ping-pong schedule (tiles 27-29). One 512-thread
-// block per CU, 8 waves as 2 (co) x 4 (px); a wave owns TM x TN outputs as four
-// quadrants (m, n) of QM x QN. Each 64-deep K tile is held in LDS as four
-// half-tile images: A half m = the quadrant-m weight rows of both co wave rows,
-// B half n = the quadrant-n pixel rows of all four px wave columns, each a
-// [rows][64] bf16 image with 128-B rows, chunk-swizzled (c ^ (row>>1 & 7)) on
-// the DMA source address and on the fragment read (guide rule 21). Two K-tile
-// buffers (2 x (BM + BN) x 128 B: 128 KB at 256 x 256).
-//
-// Per K tile a wave runs four phases, one quadrant each:
-//   read fragments (Q00: A0+B0, Q01: B1, Q11: A1, Q10: none) | issue one
-//   half-tile DMA | counted vmcnt | s_barrier | 16 MFMAs | s_barrier
-// The two co wave rows (one wave of each per SIMD) run one barrier apart, so
-// on every SIMD one wave's MFMA cluster overlaps the other wave's LDS reads
-// and DMA issue (guide §5, "the 256^2 8-phase template"). Half-tiles are
-// issued six (A0) or five (B0, B1, A1) phases before their first read, into
-// the slot their previous occupant (two K tiles earlier) has left; after every
-// phase's issue the wave retires all but its four youngest half-tiles, so
-// each half is retired >= 1 phase (two barriers) before any wave reads it.
-// Requires Cin % 64 == 0 and Cout_pad % BM == 0.
-// -------------------------------------------------------------------------
-template <int APW, int BPW, int SELF>
-__device__ __forceinline__ void p8_wait(int d) {
-#ifdef YCX_P8_NOWAIT
-  return;
-#endif
-  // d = phases past the last DMA issue (<= 0: steady state: four half-tiles in
-  // flight, less this phase's own when it is issued after the wait: SELF)
-  if (d <= 0) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * APW + 2 * BPW - SELF) : "memory");
-  } else if (d == 1) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(APW + 2 * BPW) : "memory");
-  } else if (d == 2) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(APW + BPW) : "memory");
-  } else if (d == 3) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(APW) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-}
-
-struct KDec {  // K position (tap ky, kx; channel block cb) of the next K tile a DMA series issues
-  int ky, kx, cb;
-  __device__ __forceinline__ void next(int cin, int kw) {
-    cb += 64;
-    if (cb == cin) {
-      cb = 0;
-      if (++kx == kw) { kx = 0; ++ky; }
-    }
-  }
-};
-
-template <int BM, int BN, bool DIM>  // DIM: DMA issued inside the MFMA cluster instead of the read section
-__global__ void __launch_bounds__(512) conv_bf16_p8(ConvArgs a) {
-  constexpr int TM = BM / 2, TN = BN / 4;      // wave tile (co x px)
-  constexpr int QM = TM / 2, QN = TN / 2;      // quadrant
-  constexpr int FM = QM / 16, FN = QN / 16;    // 16x16 fragments per quadrant
-  constexpr int AH = BM / 2, BH = BN / 2;      // rows per half-tile image
-  constexpr int APW = AH / 64, BPW = BH / 64;  // 1-KB DMA pieces per wave per half-tile
-  constexpr int AHB = AH * 128, BHB = BH * 128;
-  constexpr int KTB = 2 * AHB + 2 * BHB;       // one K tile
-  static_assert(APW >= 1 && BPW >= 1 && FM >= 1 && FN >= 1, "tile");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * KTB];
-
-  const elt_t* __restrict__ X = reinterpret_cast<const elt_t*>(a.x);
-  const elt_t* __restrict__ Wt = reinterpret_cast<const elt_t*>(a.w);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;  // wr: co wave row = the ping-pong group
-  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
-  const int ct = L % a.n_ct, pt = L / a.n_ct;
-  const int co0 = ct * BM, px0 = pt * BN;
-  const int lrow = lane >> 3, pch = lane & 7;
-
-  const int w_bytes = a.Cout_pad * a.Ktot * 2, x_bytes = a.N * a.H * a.W * a.in_cs * 2;
-  int a_off[2][APW];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int i = 0; i < APW; ++i) {
-      const int r = (wid + 8 * i) * 8 + lrow;           // image row
-      const int trow = (r / QM) * TM + h * QM + r % QM;  // tile row (output channel)
-      a_off[h][i] = ((co0 + trow) * a.Ktot + ((pch ^ swz<64>(r)) << 3)) * 2;
-    }
-  int b_iy0[2][BPW], b_ix0[2][BPW], b_base[2][BPW];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int i = 0; i < BPW; ++i) {
-      const int r = (wid + 8 * i) * 8 + lrow;
-      const int p = px0 + (r / QN) * TN + h * QN + r % QN;
-      const bool ok = p < a.M;
-      const int pp = ok ? p : 0;
-      const int n = pp / a.HoWo, rem = pp - n * a.HoWo;
-      const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
-      b_iy0[h][i] = ok ? oy * a.S - a.P : -(1 << 20);
-      b_ix0[h][i] = ox * a.S - a.P;
-      b_base[h][i] = (((n * a.H + b_iy0[h][i]) * a.W + b_ix0[h][i]) * a.in_cs + a.in_coff +
-                      ((pch ^ swz<64>(r)) << 3)) * 2;
-    }
-
-  auto issue_a = [&](int h, int kt) {
-#ifdef YCX_P8_NODMA
-    if (kt > 1) return;
-#endif
-    char* dst = smem + (kt & 1) * KTB + h * AHB;
-#pragma unroll
-    for (int i = 0; i < APW; ++i) buf_lds16(Wt, w_bytes, a_off[h][i], kt * 128, dst + (wid + 8 * i) * 1024);
-  };
-  auto issue_b = [&](int h, int kt, const KDec& d) {
-#ifdef YCX_P8_NODMA
-    if (kt > 1) return;
-#endif
-    char* dst = smem + (kt & 1) * KTB + 2 * AHB + h * BHB;
-    const int tap = ((d.ky * a.W + d.kx) * a.in_cs + d.cb) * 2;
-#pragma unroll
-    for (int i = 0; i < BPW; ++i) {
-      const bool ok = (unsigned)(b_iy0[h][i] + d.ky) < (unsigned)a.H && (unsigned)(b_ix0[h][i] + d.kx) < (unsigned)a.W;
-      buf_lds16(X, x_bytes, ok ? b_base[h][i] + tap : 0x7FFFFFF0, 0, dst + (wid + 8 * i) * 1024);
-    }
-  };
-
-  f32x4 acc[2][2][FM][FN];
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[m][n][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  eltx8 af[2][2][FM], bfr[2][2][FN];  // [quadrant][kk][fragment]
-
-  auto read_a = [&](int h, int buf) {
-    const char* base = smem + buf * KTB + h * AHB;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int r = wr * QM + i * 16 + (lane & 15), c = kk * 4 + (lane >> 4);
-        af[h][kk][i] = *reinterpret_cast<const eltx8*>(base + r * 128 + ((c ^ swz<64>(r)) << 4));
-      }
-  };
-  auto read_b = [&](int h, int buf) {
-    const char* base = smem + buf * KTB + 2 * AHB + h * BHB;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int r = wc * QN + j * 16 + (lane & 15), c = kk * 4 + (lane >> 4);
-        bfr[h][kk][j] = *reinterpret_cast<const eltx8*>(base + r * 128 + ((c ^ swz<64>(r)) << 4));
-      }
-  };
-  auto mfma_q = [&](int m, int n, auto&& dma) {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[m][n][i][j] = YCX_MFMA16(af[m][kk][i], bfr[n][kk][j], acc[m][n][i][j], 0, 0, 0);
-      if (DIM && kk == 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        dma();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  const int nt = a.nsteps;
-  const int last = 4 * nt - 7;  // phase of the last DMA issue (A1 of tile nt - 1)
-  KDec d0{0, 0, 0}, d1{0, 0, 0};  // next K tile of the B0 and B1 DMA series
-  // prologue = phases -6 .. -1: A0(0) B0(0) B1(0) A1(0) [A0(1) B0(1)]
-  issue_a(0, 0);
-  issue_b(0, 0, d0);
-  d0.next(a.Cin, a.KW);
-  issue_b(1, 0, d1);
-  d1.next(a.Cin, a.KW);
-  issue_a(1, 0);
-  if (nt > 1) {
-    issue_a(0, 1);
-    issue_b(0, 1, d0);
-    d0.next(a.Cin, a.KW);
-  }
-  p8_wait<APW, BPW, 0>(-1 - last);
-  __builtin_amdgcn_s_barrier();
-#ifndef YCX_P8_NOSTAGGER
-  if (wr == 1) __builtin_amdgcn_s_barrier();  // the second group runs one barrier behind
-#endif
-  __builtin_amdgcn_sched_barrier(0);
-
-  for (int u = 0; u < nt; ++u) {
-    const int buf = u & 1, j = 4 * u;
-    // Q00: A0 + B0 of tile u; issue B1(u + 1)
-    auto dma0 = [&] {
-      if (u + 1 < nt) {
-        issue_b(1, u + 1, d1);
-        d1.next(a.Cin, a.KW);
-      }
-    };
-    read_a(0, buf);
-    read_b(0, buf);
-    if (!DIM) dma0();
-    p8_wait<APW, BPW, DIM ? BPW : 0>(j - last);
-    mfma_q(0, 0, dma0);
-    // Q01: B1; issue A1(u + 1)
-    auto dma1 = [&] {
-      if (u + 1 < nt) issue_a(1, u + 1);
-    };
-    read_b(1, buf);
-    if (!DIM) dma1();
-    p8_wait<APW, BPW, DIM ? APW : 0>(j + 1 - last);
-    mfma_q(0, 1, dma1);
-    // Q11: A1; issue A0(u + 2)
-    auto dma2 = [&] {
-      if (u + 2 < nt) issue_a(0, u + 2);
-    };
-    read_a(1, buf);
-    if (!DIM) dma2();
-    p8_wait<APW, BPW, DIM ? APW : 0>(j + 2 - last);
-    mfma_q(1, 1, dma2);
-    // Q10: no reads; issue B0(u + 2)
-    auto dma3 = [&] {
-      if (u + 2 < nt) {
-        issue_b(0, u + 2, d0);
-        d0.next(a.Cin, a.KW);
-      }
-    };
-    if (!DIM) dma3();
-    p8_wait<APW, BPW, DIM ? BPW : 0>(j + 3 - last);
-    mfma_q(1, 0, dma3);
-  }
-#ifndef YCX_P8_NOSTAGGER
-  if (wr == 0) __builtin_amdgcn_s_barrier();  // same barrier count in both groups
-#endif
-  __builtin_amdgcn_sched_barrier(0);
-
-  const int cob = co0 + wr * TM, pxb = px0 + wc * TN;
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) epilogue_regs<FM, FN>(a, acc[m][n], cob + m * QM, pxb + n * QN, lane);
-}
-
-#endif  // YCX_EXPERIMENTAL_TILES
-
 // -------------------------------------------------------------------------
 // 3x3 stride-1 conv from an LDS halo tile. A block owns a 16x16 output tile of
 // one image and BM output channels. Per 64-channel input chunk the (16+2)^2
@@ -3108,9 +2853,6 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
           v[4 * i + q] = ycx_act<true>(fmaf(acc[i][j][q], qv[i][q], bv[i][q]), a.act, a.slope) * osc;
       const uint2 ov = make_uint2(f8x4_pack(v[0], v[1], v[2], v[3]), f8x4_pack(v[4], v[5], v[6], v[7]));
       const int p = pb + 16 * j;
-#ifdef YCX_F8W_NOSTORE  // development timing only: the output stores skipped (wrong results)
-      if (p < 0)
-#endif
       if (p < a.M && co < a.Cout) if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(uint2))) *reinterpret_cast<uint2*>(Y + (size_t)p * a.out_cs + co) = ov;
     }
   }
@@ -3309,8 +3051,8 @@ const TileInfo kTiles[] = {
     {256, 256, 64, "glds_co256_px256_k64_s2"},
     {256, 128, 64, "glds_co256_px128_k64_s2"},
     {128, 256, 64, "glds_co128_px256_k64_s2"},
-    {256, 256, 64, "retired_p8_co256_px256"},     // 27-33: retired experiments, built only with
-    {128, 256, 64, "retired_p8_co128_px256"},     // -DYCX_EXPERIMENTAL_TILES
+    {256, 256, 64, "retired_p8_co256_px256"},     // 27-33: retired experiments, kept in
+    {128, 256, 64, "retired_p8_co128_px256"},     // tools/experiments/pingpong_p8_tiles27_33.patch
     {256, 128, 64, "retired_p8_co256_px128"},
     {256, 256, 64, "retired_p8i_co256_px256"},
     {128, 256, 64, "retired_p8i_co128_px256"},
@@ -3404,16 +3146,13 @@ ycx_status launch_halo(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
-// Channel groups of the XCD region map (ycx_tile_of) for an LDS-DMA tile launch.
-// YCX_GLDS_GC (development A/B) forces one value for every launch.
-int glds_gc(const ConvArgs& a) {
-  static const int forced = [] {
-    const char* e = getenv("YCX_GLDS_GC");
-    return e ? atoi(e) : -1;
-  }();
-  if (forced >= 0) return forced;
-  return 0;
-}
+// Channel groups of the XCD region map (ycx_tile_of) for an LDS-DMA tile launch: 0 (plain
+// bijective XCD remap). The region map (gc 2 / 4) measured slower in the concurrent bench
+// (DESIGN.md §6 r03); -DYCX_GLDS_GC=<g> builds it for an A/B.
+#ifndef YCX_GLDS_GC
+#define YCX_GLDS_GC 0
+#endif
+static inline int glds_gc(const ConvArgs&) { return YCX_GLDS_GC; }
 
 template <int BM, int BN, int WM, int WN, bool TT = false, int NST = 3, int NSB = NST>
 ycx_status launch_glds(ConvArgs a, hipStream_t st) {
@@ -3481,18 +3220,6 @@ ycx_status launch_f8(ConvArgs a, hipStream_t st) {
   else hipLaunchKernelGGL((conv_f8_glds<BM, BN, WM, WN, 0>), g, b, 0, st, a, HeadArgs{});
   return ycx_launch_status();
 }
-
-#ifdef YCX_EXPERIMENTAL_TILES
-template <int BM, int BN, bool DIM = false>
-ycx_status launch_p8(ConvArgs a, hipStream_t st) {
-  if (a.Cin % 64 != 0 || a.Cout_pad % BM != 0) return YCX_ERR_UNSUPPORTED;
-  a.nsteps = a.KH * a.KW * (a.Cin / 64);
-  a.n_ct = a.Cout_pad / BM;
-  a.nwg = a.n_ct * ((a.M + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_bf16_p8<BM, BN, DIM>), dim3(a.nwg), dim3(512), 0, st, a);
-  return ycx_launch_status();
-}
-#endif
 
 // Weight-resident 1x1 (tile 22): the wave split follows cout_pad, the K unroll Cin.
 template <int WCO, int WPX, int TPW, int NS, int SUB>
@@ -3683,15 +3410,13 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
     if (d->cout_pad == 64 && d->ho >= 160) return 19;
   }
   // 3x3/s2 64 -> 128 downsample with >= 4 output tiles per persistent block: weights in
-  // registers, input halo in LDS (tile 50; YCX_NO_S2WSR=1 keeps the im2col tiles for A/B)
+  // registers, input halo in LDS (tile 50)
   if (allow_wres && d->kh == 3 && d->kw == 3 && d->stride == 2 && d->pad == 1 && d->cin == 64 &&
       d->cout_pad == 128 && d->out_layout == YCX_OUT_NHWC && d->ho % 4 == 0 && d->wo % 16 == 0 &&
       (long long)d->n * (d->ho / 4) * (d->wo / 16) >= 2048) {
-    static const bool off = [] {
-      const char* e = getenv("YCX_NO_S2WSR");
-      return e && atoi(e) != 0;
-    }();
-    if (!off) return 50;
+#ifndef YCX_NO_S2WSR  // -DYCX_NO_S2WSR: the im2col tiles instead, for an A/B build
+    return 50;
+#endif
   }
   // 40-wide maps (not 16-aligned): the 8 x 40 band halo tile where it has >= 2.5 waves of
   // workgroups (40^2 bs 32 256->512: 0.113 vs 0.124 ms; with fewer workgroups it loses to tile 16,
@@ -3831,15 +3556,6 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x,
     case 48: return launch_halo<64, 2, 4, 2, 8, 40>(a, st);      // band halo tiles (40-wide maps)
     case 49: return launch_halo<128, 4, 2, 2, 4, 40>(a, st);
     case 50: return launch_s2wsr(a, st);
-#ifdef YCX_EXPERIMENTAL_TILES  // retired experiments (tools/build_variant.sh NAME -DYCX_EXPERIMENTAL_TILES)
-    case 27: return launch_p8<256, 256>(a, st);
-    case 28: return launch_p8<128, 256>(a, st);
-    case 29: return launch_p8<256, 128>(a, st);
-    case 30: return launch_p8<256, 256, true>(a, st);
-    case 31: return launch_p8<128, 256, true>(a, st);
-    case 32: return launch_glds<128, 128, 2, 2, false, 2>(a, st);
-    case 33: return launch_glds<64, 128, 1, 4, false, 2>(a, st);
-#endif
     default: return YCX_ERR_UNSUPPORTED;
   }
 }

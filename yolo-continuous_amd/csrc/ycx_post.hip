@@ -491,7 +491,7 @@ extern "C" ycx_status ycx_decode_filter(const ycx_decode_filter_desc* d, const f
   DecodeFilterArgs a;
   a.d = *d;
   for (int l = 0; l < 4; ++l) a.heads[l] = l < d->nl ? heads[l] : nullptr;
-  bool quad = getenv("YCX_DECODE_SCALAR") == nullptr;  // A/B switch
+  bool quad = true;  // the one-row-per-thread kernel covers ragged levels and unaligned heads
   for (int l = 0; l < d->nl; ++l)
     quad = quad && (d->h[l] * d->w[l]) % 4 == 0 && (reinterpret_cast<uintptr_t>(heads[l]) & 15) == 0;
   if (quad) {

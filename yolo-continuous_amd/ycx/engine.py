@@ -452,7 +452,7 @@ class Engine:
     """A compiled plan bound to device memory for one (input shape, device, precision)."""
 
     def __init__(self, model, shape, device, precision='bf16', fuse_stem2=True, fp8_amax=None, prepacked=None,
-                 fuse_pool=True):
+                 fuse_pool=True, fuse_pair=True):
         if device.type != 'cuda':
             raise RuntimeError("ycx: the HIP path needs the model input on a ROCm device (tensor.to('cuda')); "
                                "there is no CPU path")
@@ -463,6 +463,7 @@ class Engine:
         self.dt = {'bf16': L.DT_BF16, 'f32': L.DT_F32, 'fp8': L.DT_FP8, 'fp16': L.DT_F16}[precision]
         self.fuse_stem2 = fuse_stem2
         self.fuse_pool = fuse_pool  # False: every pool writes its map (fp8 calibration reads them all)
+        self.fuse_pair = fuse_pair  # False: every 1x1 of a pair stores its map (fp8 calibration reads them all)
         self.prepacked = prepacked  # {'p<i>': packed tensor} from ycx.prepack (skips folding / packing)
         self.graph_exec = None
         self.graph, self.out_vals, self.is_list = self.plan.graph, self.plan.out_vals, self.plan.is_list
@@ -572,7 +573,7 @@ class Engine:
         also feeding the MP branch). 16-bit plans; YCX_NO_CONV_PAIR=1 keeps them apart.
         Returns {id(first conv): second conv}."""
         out = {}
-        if not self.h16 or os.environ.get('YCX_NO_CONV_PAIR'):
+        if not self.h16 or not self.fuse_pair or os.environ.get('YCX_NO_CONV_PAIR'):
             return out
         taken = set()
 
@@ -590,11 +591,15 @@ class Engine:
                 continue
             if x.n * x.h * x.w < 8 * 64 * 256 or (x.role != 'input' and (x.coff % 8 or x.buf.c % 8)):
                 continue
+            if len(v.consumers) > 1 and (v.coff % 8 or v.buf.c % 8):  # y1 is stored: ycx_conv2d_pair's 16-B stores
+                continue
             for b in v.consumers:
                 if not pointwise(b) or b.inputs[0] is not v or id(b) in taken or id(b) in out:
                     continue
                 cb = int(b.p['w'].shape[0])
                 if self._cout_pad(cb) not in (128, 256) or cb % 8:
+                    continue
+                if b.out.role == 'act' and (b.out.coff % 8 or b.out.buf.c % 8):
                     continue
                 out[id(a)] = b
                 taken.update((id(a), id(b)))
@@ -625,6 +630,12 @@ class Engine:
     def _build(self):
         dev, dt = self.device, self.dtype
         self.buffers, self.params = [], []
+        # packed tensors are named by the conv's position among the graph's conv / stem nodes,
+        # not by packing order: which convs fuse (stem pair, 1x1 pair) varies with the batch
+        # size and the A/B switches, and a prepack file is reused at any batch size
+        self.packed = {}
+        self._conv_index = {id(nd): i for i, nd in enumerate(
+            nd for nd in self.graph.nodes if nd.kind in ('conv', 'stem'))}
         pairs = self._stem2_pairs()
         fused = {id(c) for c in pairs.values()}
         for b in self.activation_bufs():  # the stem maps of fused stem2 pairs stay in LDS
@@ -697,8 +708,8 @@ class Engine:
         else:     # [cout_pad][kh][kw][cin] in the activation dtype
             wshape, wdt = (cpad, k, k, cin), self.dtype
         bshape = (2 * cpad,) if (f8 and not stem and not bf16_weights) else (cpad,)
+        i = 2 * self._conv_index[id(node)]
         if self.prepacked is not None:
-            i = len(self.params)
             wt, bt = self.prepacked.get(f"p{i}"), self.prepacked.get(f"p{i + 1}")
             if wt is None or bt is None or tuple(wt.shape) != wshape or wt.dtype != wdt or \
                     tuple(bt.shape) != bshape or bt.dtype != torch.float32:
@@ -721,6 +732,7 @@ class Engine:
         wt = wt.to(self.device)
         bt = bt.to(self.device)
         self.params += [wt, bt]
+        self.packed[f"p{i}"], self.packed[f"p{i + 1}"] = wt, bt
         d = L.ConvDesc()
         d.n, d.h, d.w, d.cin = x.n, x.h, x.w, cin
         if x.role == 'input':

@@ -205,11 +205,18 @@ class Model(nn.Module):
             raise RuntimeError("ycx: Model is inference-only on the HIP path (training is out of scope); "
                                "call .eval() first")
         outs = self.engine_for(x.shape, x.device, slot=self.EAGER_SLOT).run(x)
-        if self.precision == 'fp16' and not _all_finite(outs):
+        if self.precision == 'fp16' and not _all_finite(outs) and _all_finite(x):
             # the fp16 range guard: an activation past 65504 became inf at its producer's store and
-            # reached the heads as inf / NaN. The reference's fp32 forward has no such limit: re-plan
-            # in bf16 (fp32's exponent range, 8-bit significand) for this and every later call.
+            # reached the heads as inf / NaN (a non-finite input is passed through, as the
+            # reference's fp32 forward does). The reference's fp32 forward has no such limit:
+            # re-plan in bf16 (fp32's exponent range, 8-bit significand) for this and every later call.
             import warnings
+            if (self.precision,) + tuple(int(v) for v in x.shape[2:]) in self._prepacked:
+                # a bf16 re-plan would fold this module's own parameters, not the prepacked ones
+                warnings.warn("ycx: the fp16 plan overflowed (non-finite head logits) on prepacked weights; "
+                              "returning them as they are (re-pack in 'bf16' or 'f32' for this checkpoint)",
+                              RuntimeWarning, stacklevel=2)
+                return outs
             warnings.warn("ycx: the fp16 plan overflowed (non-finite head logits: an activation exceeds "
                           "65504); switching this Model to precision='bf16' (about 1e-3 relative error, "
                           "use 'f32' for the 1e-3 parity mode)", RuntimeWarning, stacklevel=2)
@@ -292,7 +299,9 @@ class Model(nn.Module):
             images = synthetic_images(n, self.image_chan, int(hw[0]), int(hw[1]), seed=seed)
         dev = torch.device(device) if device is not None else images.device
         images = images.to(dev, torch.float32).contiguous()
-        eng = Engine(self, tuple(images.shape), dev, 'bf16', fuse_pool=False)  # the fp8 plan's fusions
+        # every buffer the fp8 plan stores must be written here: no fused MP pools, no 1x1 pairs
+        # (a pair whose first output has one consumer keeps it on chip and never stores it)
+        eng = Engine(self, tuple(images.shape), dev, 'bf16', fuse_pool=False, fuse_pair=False)
         try:
             eng.run(images)
             amax = [dict(c=int(b.c), amax=float(b.tensor.abs().max().float())) for b in eng.activation_bufs()]

@@ -8,8 +8,10 @@ dequantisation vector for fp8 (``ycx/engine.py``). This module stores that
 result, with the fp8 calibration record it depends on, in one safetensors file
 so a serving process skips the host-side folding and calibration.
 
-The file holds one plan (precision, input H x W): tensors ``p0, p1, ...`` in the
-engine's packing order and ``metadata['ycx']`` = JSON {format, precision, hw,
+The file holds one plan (precision, input H x W): tensors ``p<2i>, p<2i+1>`` =
+the packed weights and bias of the i-th conv / stem node of the lowered graph
+(named by node, not by packing order, so the fusions that vary with the batch
+size -- the 1x1 pair -- cannot permute them) and ``metadata['ycx']`` = JSON {format, precision, hw,
 n_tensors, fp8_amax, state_dict_sha256}. The batch size is free: packed weights
 do not depend on it. Loading checks every tensor's shape and dtype against the
 plan it is bound to, and refuses a file written for another plan.
@@ -27,7 +29,7 @@ import json
 
 import torch
 
-FORMAT = "ycx-prepack-2"  # 2 (r04): fused 1x1 pairs pack their two weight sets back to back
+FORMAT = "ycx-prepack-3"  # 3 (r05): tensors named by conv node (2i, 2i+1), independent of which convs fuse
 
 
 def state_dict_sha256(model):
@@ -46,7 +48,7 @@ def save(model, path, hw, precision=None, device="cuda"):
     model.set_precision(precision)
     try:
         eng = model.engine_for((1, model.image_chan, int(hw[0]), int(hw[1])), device)
-        tensors = {f"p{i}": t.detach().cpu().contiguous() for i, t in enumerate(eng.params)}
+        tensors = {k: t.detach().cpu().contiguous() for k, t in eng.packed.items()}
         meta = dict(format=FORMAT, precision=precision, hw=[int(hw[0]), int(hw[1])], n_tensors=len(tensors),
                     fp8_amax=model._fp8_amax.get((int(hw[0]), int(hw[1]))) if precision == "fp8" else None,
                     state_dict_sha256=state_dict_sha256(model))
@@ -81,7 +83,7 @@ def main(argv=None):
     ap.add_argument("--anchors", default="12,16,19,36,40,28,36,75,76,55,72,146,142,110,192,243,459,401")
     ap.add_argument("--weights", help="state_dict file (torch.save of Model.state_dict(); loaded weights_only)")
     ap.add_argument("--size", type=int, default=640)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "f32", "fp8"])
+    ap.add_argument("--precision", default="bf16", choices=["fp16", "bf16", "f32", "fp8"])
     ap.add_argument("--calib", help="fp8: a tensor file of calibration images [N, 3, H, W] fp32 in [0, 1]")
     ap.add_argument("--out", required=True)
     args = ap.parse_args(argv)
