@@ -99,6 +99,10 @@ def parse(argv=None):
     ap.add_argument("--image-in-steps", type=int, default=30,
                     help="image-in leg (SURVEY 8(d) H2D-inclusive variant): seeded 512x773 uint8 BGR host images "
                          "in pinned memory -> H2D -> ycx_letterbox_batch -> the same path; 0: skip")
+    ap.add_argument("--fp16-steps", type=int, default=None,
+                    help="the north_star-conforming fp16 plan (1e-3 on box / confidence tensors) timed in the same "
+                         "run after the headline leg, same steps and mode (default: --steps when --precision is "
+                         "bf16; 0: skip); reported as value_fp16 / ms_per_step_fp16 / roofline_fp16")
     ap.add_argument("--round", default=None,
                     help="profiles/<round>/traffic.json for roofline.traffic (default: the newest round that has one)")
     ap.add_argument("--dry-run", action="store_true",
@@ -567,6 +571,104 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def timed_leg(args, det, mode, dist_on, gather, lat_ev, steps=None, latency_steps=None):
+    """W untimed warm-up steps, then exactly ``steps`` timed steps between a barrier +
+    device synchronise on both sides (host wall clock), then the unloaded latency leg.
+    Returns (elapsed s, loaded per-batch latencies ms, unloaded latencies ms, last kc)."""
+    from ycx.dist import gather_detections
+    steps = args.steps if steps is None else steps
+    latency_steps = args.latency_steps if latency_steps is None else latency_steps
+    pipeline = mode != "serial"
+
+    def step(i=None):
+        timing = lat_ev[i] if i is not None else None
+        if mode == "concurrent":  # the collective on the batch's own stream, issued in batch order on every rank
+            dets, keep, kc, done = det.submit(timing=timing, then=gather if dist_on else None,
+                                              post=not args.diag_forward_only)
+            return kc
+        if pipeline:
+            dets, keep, kc, _ = det.submit(timing=timing)
+            if dist_on:  # the single collective, on the post stream after this batch's NMS
+                with torch.cuda.stream(det.s_post):
+                    dets, kc, keep = gather_detections(dets, kc, keep)
+            return kc
+        if timing is not None:
+            timing[0].record()
+        dets, keep, kc = det()
+        if dist_on:  # the single collective: all-gather of padded detections (+ counts, keep rows)
+            dets, kc, keep = gather_detections(dets, kc, keep)
+        if timing is not None:
+            timing[1].record()
+        return kc
+
+    def drain():
+        if pipeline:
+            det.synchronize()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    drain()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        kc = step(i)
+    drain()
+    if dist_on:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    det.check()  # outside the timed region: no batch left the plan's range (fp16: |a| <= 65504)
+    lat = [a.elapsed_time(b) for a, b in lat_ev]
+    # unloaded latency: one batch in flight at a time (input resident -> detections, + gather)
+    lat1 = []
+    for _ in range(latency_steps):
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        step()
+        drain()
+        lat1.append((time.perf_counter() - t1) * 1e3)
+    return elapsed, lat, lat1, kc
+
+
+def precision_leg(args, dev, rank, world, dist_on, gather, mode, precision, steps):
+    """A second plan of the same workload in another precision, timed exactly as the
+    headline leg (warm-up, ``steps`` timed steps between barriers, max over ranks) in the
+    same run: the fp16 plan is the one that holds north_star's 1e-3 on box / confidence
+    tensors (detect.py:227-231 compares the reference's fp32 outputs). Returns the
+    ``*_<precision>`` keys of the JSON line."""
+    import copy
+    a = copy.copy(args)
+    a.precision = precision
+    pipeline = False if mode == "serial" else mode
+    _, det, _, _, _ = setup(a, dev, rank, pipeline=pipeline)
+    lat_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    elapsed, lat, _, _ = timed_leg(a, det, mode, dist_on, gather, lat_ev, steps=steps, latency_steps=0)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist_on:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    value = world * args.batch * steps / elapsed
+    det1 = det.slots[0] if pipeline else det
+    rl = roofline(det1, args.roofline_steps, precision) if rank == 0 else None
+    det.close()
+    sfx = "_" + precision
+    out = {"value" + sfx: round(value, 2), "ms_per_step" + sfx: round(elapsed / steps * 1e3, 4),
+           "steps" + sfx: steps, "p50_ms" + sfx: round(statistics.median(lat), 4)}
+    if rl is not None:
+        peak = PEAK[precision]
+        out["roofline" + sfx] = {"bound": "mfma", "kernel": rl['kernel'], "achieved": round(rl['achieved'], 2),
+                                 "peak": peak, "unit": "TFLOP/s", "frac": round(rl['achieved'] / peak, 4),
+                                 "avg_launch_ms": round(rl['avg_launch_ms'], 5),
+                                 "flops_per_launch": int(rl['flops_per_launch']),
+                                 "forward_kernel_ms": round(rl['forward_kernel_ms'], 4),
+                                 "forward_floor_ms": round(rl['forward_floor_ms'], 4)}
+    return out
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -609,57 +711,7 @@ def main(argv=None):
         g_dets, g_kc, g_keep = gather_detections(dets, kc, keep)
         return g_dets, g_keep, g_kc
 
-    def step(i=None):
-        timing = lat_ev[i] if i is not None else None
-        if mode == "concurrent":  # the collective on the batch's own stream, issued in batch order on every rank
-            dets, keep, kc, done = det.submit(timing=timing, then=gather if dist_on else None,
-                                              post=not args.diag_forward_only)
-            return kc
-        if pipeline:
-            dets, keep, kc, _ = det.submit(timing=timing)
-            if dist_on:  # the single collective, on the post stream after this batch's NMS
-                with torch.cuda.stream(det.s_post):
-                    dets, kc, keep = gather_detections(dets, kc, keep)
-            return kc
-        if timing is not None:
-            timing[0].record()
-        dets, keep, kc = det()
-        if dist_on:  # the single collective: all-gather of padded detections (+ counts, keep rows)
-            dets, kc, keep = gather_detections(dets, kc, keep)
-        if timing is not None:
-            timing[1].record()
-        return kc
-
-    def drain():
-        if pipeline:
-            det.synchronize()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        step()
-    drain()
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        kc = step(i)
-    drain()
-    if dist_on:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    det.check()  # outside the timed region: no batch left the plan's range (fp16: |a| <= 65504)
-    lat = [a.elapsed_time(b) for a, b in lat_ev]
-    # unloaded latency: one batch in flight at a time (input resident -> detections, + gather)
-    lat1 = []
-    for _ in range(args.latency_steps):
-        if dist_on:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        step()
-        drain()
-        lat1.append((time.perf_counter() - t1) * 1e3)
+    elapsed, lat, lat1, kc = timed_leg(args, det, mode, dist_on, gather, lat_ev)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -670,6 +722,14 @@ def main(argv=None):
 
     img_in = image_in_leg(args, det, dev, dist_on, gather) if args.image_in_steps > 0 else None
     rl = roofline(det1, args.roofline_steps, args.precision) if rank == 0 else None
+    flops_per_image = det1.engine.flops_per_image
+    detections_last_step = int(kc.sum().item())
+    n16 = args.fp16_steps if args.fp16_steps is not None else (args.steps if args.precision == "bf16" else 0)
+    fp16 = None
+    if n16 > 0 and args.precision != "fp16" and not args.diag_forward_only:
+        det.close()  # the headline plan's HBM back before the second plan is built
+        del det, det1, model
+        fp16 = precision_leg(args, dev, rank, world, dist_on, gather, mode, "fp16", n16)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, sd, cfg)
@@ -692,7 +752,7 @@ def main(argv=None):
                        "latency": "p50_ms: submit -> detections of a batch in the timed loop (batches_in_flight "
                                   "queued); p50_ms_unloaded: host wall time of one batch alone, synchronised",
                        "conf_thres": args.conf, "iou_thres": args.iou, "max_det": args.max_det},
-            "mfma_fraction_whole_step": round(det1.engine.flops_per_image * value /
+            "mfma_fraction_whole_step": round(flops_per_image * value /
                                               (world * peak * 1e12), 4),
             "roofline": {"bound": "mfma", "kernel": rl['kernel'], "achieved": round(rl['achieved'], 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(rl['achieved'] / peak, 4),
@@ -713,7 +773,8 @@ def main(argv=None):
             "cpu_baseline": cpu,
             "rccl_world_size": dist.get_world_size() if dist_on else 1,
             **(img_in or {}),
-            "detections_last_step": int(kc.sum().item()),
+            **(fp16 or {}),
+            "detections_last_step": detections_last_step,
         }
         print(json.dumps(out), flush=True)
         if os.environ.get("YCX_BENCH_KERNELS"):  # the per-op roofline gap table (serial leg, HIP events)
