@@ -2153,7 +2153,7 @@ __device__ __forceinline__ int s2_swz(int col) { return (col ^ ((col >> 1) & 2))
 constexpr int s2_pad(int v, int m) { return v + ((m - v % 32) + 32) % 32; }  // smallest >= v, == m mod 32
 
 template <int SS, int ACT1, int ACT2, bool F8 = false>  // stem stride, stem / conv act, e4m3 output
-__global__ void __launch_bounds__(256, 2) stem2_fused(ConvArgs sa, ConvArgs ca) {
+__global__ void __launch_bounds__(256, SS == 1 ? 2 : 1) stem2_fused(ConvArgs sa, ConvArgs ca) {  // SS 2: 100 KB of LDS, one block per CU
   constexpr int NPIX = kS2R * kS2C, NGRP = (NPIX + 15) / 16, GPW = (NGRP + 3) / 4;
   constexpr int IR = (kS2R - 1) * SS + 3, IC = (kS2C - 1) * SS + 3;  // image patch rows / cols
   constexpr int RS = s2_pad(IC, 7), CPS = s2_pad(IR * RS, 23);         // padded row / plane strides
