@@ -42,7 +42,7 @@ SHAPES = [  # n, h, w, cin, cout, k, s
     (32, 20, 20, 512, 1024, 3, 1),
     (32, 40, 40, 256, 512, 3, 1),
 ]
-# CONV_EXTRA="64,32,32,4096,4096,1,1;32,40,40,1024,1024,1,1": extra shapes appended (indices continue)
+# CONV_ACT=0|1|2: the activation (default SiLU). CONV_EXTRA="64,32,32,4096,4096,1,1;32,40,40,1024,1024,1,1": extra shapes appended (indices continue)
 for _s in filter(None, os.environ.get("CONV_EXTRA", "").split(";")):
     SHAPES.append(tuple(int(v) for v in _s.split(",")))
 
@@ -65,7 +65,7 @@ def run(shape, tile, iters=20):
     d.n, d.h, d.w, d.cin, d.in_c_off, d.in_c_stride = n, h, w, cin, 0, cin
     d.ho, d.wo, d.cout, d.cout_pad, d.out_c_off, d.out_c_stride = ho, wo, cout, cpad, 0, cout
     d.kh = d.kw = k
-    d.stride, d.pad, d.act, d.dtype, d.out_layout, d.tile = s, p, L.ACT_SILU, L.DT_BF16, L.OUT_NHWC, tile
+    d.stride, d.pad, d.act, d.dtype, d.out_layout, d.tile = s, p, int(os.environ.get("CONV_ACT", L.ACT_SILU)), L.DT_BF16, L.OUT_NHWC, tile
     st = L.stream_handle(dev)
     args = (ctypes.byref(d), x.data_ptr(), wt.data_ptr(), b.data_ptr(), y.data_ptr(), None, st)
     rc = L.lib.ycx_conv2d(*args)

@@ -49,7 +49,7 @@ def run(shape, tile, iters=20):
     d.n, d.h, d.w, d.cin, d.in_c_off, d.in_c_stride = n, h, w, cin, 0, cin
     d.ho, d.wo, d.cout, d.cout_pad, d.out_c_off, d.out_c_stride = ho, wo, cout, cpad, 0, cout
     d.kh = d.kw = k
-    d.stride, d.pad, d.act, d.dtype, d.out_layout, d.tile = s, p, L.ACT_SILU, L.DT_FP8, L.OUT_NHWC, tile
+    d.stride, d.pad, d.act, d.dtype, d.out_layout, d.tile = s, p, int(os.environ.get("CONV_ACT", L.ACT_SILU)), L.DT_FP8, L.OUT_NHWC, tile
     d.out_scale, d.res_scale = 1.0, 1.0
     st = L.stream_handle(dev)
     args = (ctypes.byref(d), x.data_ptr(), wt.data_ptr(), b.data_ptr(), y.data_ptr(), None, st)

@@ -1175,6 +1175,7 @@ __device__ __forceinline__ void epilogue_f8(const ConvArgs& a, const f32x4 (&acc
       }
     return;
   }
+  const float nl2e = silu_nl2e();
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int co = cob + i * 16 + (lane >> 4) * 4;
@@ -1185,9 +1186,9 @@ __device__ __forceinline__ void epilogue_f8(const ConvArgs& a, const f32x4 (&acc
     for (int j = 0; j < FN; ++j) {
       const int p = pxb + j * 16 + (lane & 15);
       if (p >= a.M) continue;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = ycx_act<true>(fmaf(acc[i][j][r], qv[r], bv[r]), a.act, a.slope);
+      // packed fma + act4: bit-identical to fmaf + ycx_act<true>
+      const f32x4 x = act4(__builtin_elementwise_fma(acc[i][j], qv, bv), a.act, a.slope, nl2e);
+      float v[4] = {x[0], x[1], x[2], x[3]};
       store4_f8(a, p, co, v);
     }
   }
@@ -2523,13 +2524,16 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
     // epilogue from registers: no global loads here (one would make the compiler drain vmcnt)
     const int pb = (t0 + tl) * PT + wp * TPW + (lane & 15);
     const int co = cob + 8 * (lane >> 4);  // channels co .. co+7 (cout % 8 == 0: all valid or none)
+    const float nl2e = silu_nl2e();  // act4: the packed form of ycx_act<true>, bit-identical
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       eltx8 ov;
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i) {
+        const f32x4 v = act4(acc[i][j] + bv[i], a.act, a.slope, nl2e);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)ycx_act<true>(acc[i][j][q] + bv[i][q], a.act, a.slope);
+        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)v[q];
+      }
       const int p = pb + 16 * j;
       if (p < a.M && co < a.Cout) if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov;
     }
@@ -2671,13 +2675,16 @@ __global__ void __launch_bounds__(512) conv1x1_wres_pair(ConvArgs a, ConvArgs b)
     const int pt0 = (t0 + tl) * PT;
     const int co = cob + 8 * (lane >> 4);  // channels co .. co+7
     const int s1 = co >> 6, c1 = (co >> 3) & 7;
+    const float nl2e = silu_nl2e();  // act4: the packed form of ycx_act<true>, bit-identical
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       eltx8 ov;
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i) {
+        const f32x4 v = act4(acc[i][j] + bv[i], a.act, a.slope, nl2e);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)ycx_act<true>(acc[i][j][q] + bv[i][q], a.act, a.slope);
+        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)v[q];
+      }
       const int row = j * 16 + (lane & 15), p = pt0 + row;
       if (store1 && p < a.M)
         if (YCX_OUT_OK(a, Y1 + (size_t)p * a.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y1 + (size_t)p * a.out_cs + co) = ov;
@@ -2713,9 +2720,11 @@ __global__ void __launch_bounds__(512) conv1x1_wres_pair(ConvArgs a, ConvArgs b)
     for (int j = 0; j < FN2; ++j) {
       eltx8 ov;
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i) {
+        const f32x4 v = act4(acc2[i][j] + bv2[i], b.act, b.slope, nl2e);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)ycx_act<true>(acc2[i][j][q] + bv2[i][q], b.act, b.slope);
+        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)v[q];
+      }
       const int p = pt0 + h2 * 16 * FN2 + j * 16 + (lane & 15);
       if (p < b.M && co2 < b.Cout)
         if (YCX_OUT_OK(b, Y2 + (size_t)p * b.out_cs + co2, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y2 + (size_t)p * b.out_cs + co2) = ov;
@@ -2843,14 +2852,16 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
     // epilogue from registers: no global loads here (one would make the compiler drain vmcnt)
     const int pb = (t0 + tl) * PT + wp * TPW + (lane & 15);
     const int co = cob + 8 * (lane >> 4);  // channels co .. co+7 (cout % 8 == 0: all valid or none)
+    const float nl2e = silu_nl2e();  // act4 and a packed fma: bit-identical to fmaf + ycx_act<true>
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       float v[8];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i) {
+        const f32x4 x = act4(__builtin_elementwise_fma(acc[i][j], qv[i], bv[i]), a.act, a.slope, nl2e) * osc;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          v[4 * i + q] = ycx_act<true>(fmaf(acc[i][j][q], qv[i][q], bv[i][q]), a.act, a.slope) * osc;
+        for (int q = 0; q < 4; ++q) v[4 * i + q] = x[q];
+      }
       const uint2 ov = make_uint2(f8x4_pack(v[0], v[1], v[2], v[3]), f8x4_pack(v[4], v[5], v[6], v[7]));
       const int p = pb + 16 * j;
       if (p < a.M && co < a.Cout) if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(uint2))) *reinterpret_cast<uint2*>(Y + (size_t)p * a.out_cs + co) = ov;
