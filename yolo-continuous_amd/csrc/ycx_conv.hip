@@ -780,16 +780,38 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   int i_ky = 0, i_kx = 0, i_cb = 0;  // K position (first tap) of the next stage to issue
   const int ntaps = a.KH * a.KW;
   int i_tap = 0;
+  // Stride-2 3x3s (Cin % 64 == 0) walk K channel-chunk-major with the taps that read the same
+  // input pixels next to each other: (ky, kx) = (0,0) (0,2) (0,1) (2,0) (2,2) (2,1) (1,0) (1,2) (1,1)
+  // (kx 0 / 2 of neighbouring output pixels share the odd input columns, ky 0 / 2 of neighbouring
+  // output rows the odd input rows). In (tap, chunk) order a tap's re-read of a pixel came 4-12 K
+  // steps after its first read at Cin 128 (up to 48 at Cin 512), long enough for the concurrent
+  // tiles of an XCD to evict it from the 4 MB L2: 1.9-2.5x the input bytes came from beyond the
+  // L2 (tests/probes/pmc_s2.sh). Step s is chunk s / 9, tap kTapS2[s % 9]; A follows the same K.
+  const bool kcm = !TT && !POOL && a.S == 2 && a.KH == 3 && a.KW == 3 && a.Cin == 128;
+  constexpr unsigned long long kTapS2 = 0x453786201ull;  // 4 bits per position: taps 0 2 1 6 8 7 3 5 4
+  auto k_of = [&](int s) {  // K element offset of step s in the packed weight row
+    if (!kcm) return s * BK;
+    const int c = s / 9, tp = (int)((kTapS2 >> (4 * (s - 9 * c))) & 15);
+    return tp * a.Cin + c * BK;
+  };
+  int i_s = 0;  // kcm: B steps issued
   auto a_slot = [&](int buf) { return SPLIT ? smem + buf * A_BYTES : smem + buf * STAGE; };
   auto b_slot = [&](int buf) { return SPLIT ? smem + NST * A_BYTES + buf * B_BYTES : smem + buf * STAGE + A_BYTES; };
   auto issueA = [&](int s, int buf) {
     char* base = a_slot(buf);
 #pragma unroll
-    for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * (BK * 2), base + (wid + NW * i) * 1024);
+    for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], k_of(s) * 2, base + (wid + NW * i) * 1024);
   };
-  auto issueB = [&](int buf) {  // the next K step in (tap, channel) order
+  auto issueB = [&](int buf) {  // the next K step in (tap, channel) order (kcm: k_of's order)
     char* base = b_slot(buf);
     int ky = i_ky, kx = i_kx;
+    if (!TT && !POOL && kcm) {
+      const int c = i_s / 9, tp = (int)((kTapS2 >> (4 * (i_s - 9 * c))) & 15);
+      ky = tp / 3;
+      kx = tp - 3 * ky;
+      i_cb = c * BK;
+      ++i_s;
+    }
     if (TT) {
       // second tap of the pair; past the last tap it can never pass the bounds test
       int ky1 = i_ky, kx1 = i_kx + 1;
