@@ -1238,7 +1238,7 @@ __global__ void __launch_bounds__(WM * WN * 64, POOL ? 4 : 1) conv_f8_glds(ConvA
 
   const uint8_t* __restrict__ X = reinterpret_cast<const uint8_t*>(a.x);
   const uint8_t* __restrict__ Wt = reinterpret_cast<const uint8_t*>(a.w);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
   int ct, pt;
@@ -1286,8 +1286,21 @@ __global__ void __launch_bounds__(WM * WN * 64, POOL ? 4 : 1) conv_f8_glds(ConvA
   int cb = TPS == 0 ? 16 * lch - tsel * a.Cin : 0;
   auto issueA = [&](int s, int buf) {
     char* base = smem + buf * STAGE;
+    if constexpr (POOL) {  // the weight-row offsets rebuilt per step from an opaque lane id, as the fragment addresses
+      int l = lane;
+      asm volatile("" : "+v"(l));
+      const int lr = l >> 3, pc = l & 7;
 #pragma unroll
-    for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * RB, base + (wid + NW * i) * 1024);
+      for (int i = 0; i < A_PW; ++i) {
+        const int row = 8 * (wid + NW * i) + lr;
+        const int f = (row % TM) >> 4, m = row & 15;
+        const int ch = perm ? (row / TM) * TM + 32 * (f >> 1) + 8 * (m >> 2) + 4 * (f & 1) + (m & 3) : row;
+        buf_lds16(Wt, w_bytes, (co0 + ch) * a.Ktot + ((pc ^ swz8(row)) << 4), s * RB, base + (wid + NW * i) * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_PW; ++i) buf_lds16(Wt, w_bytes, a_off[i], s * RB, base + (wid + NW * i) * 1024);
+    }
   };
   // POOL: the window's four 16-byte rows of the next K step in flight in registers, pooled
   // into LDS after the MFMAs (no VALU on them before, which would wait for the loads)
@@ -1367,7 +1380,6 @@ __global__ void __launch_bounds__(WM * WN * 64, POOL ? 4 : 1) conv_f8_glds(ConvA
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nt = a.nsteps;
-  const int c0 = 2 * (lane >> 4);
   if constexpr (POOL) {
     issueA(0, 0);
     loadB();
@@ -1389,27 +1401,48 @@ __global__ void __launch_bounds__(WM * WN * 64, POOL ? 4 : 1) conv_f8_glds(ConvA
     }
     const char* A = smem + (t & 1) * STAGE;
     const char* B = A + A_BYTES;
-    i32x8 af[FM], bfr[FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int row = wm * TM + i * 16 + (lane & 15);
+    // POOL keeps the next step's window rows (8 B_PW VGPRs) live across the MFMAs: there the A
+    // fragments come in two halves, the second half's LDS reads issued behind the first half's
+    // MFMAs, so the loop fits the 128 VGPRs of two blocks per CU
+    constexpr int AH = POOL ? 2 : 1, FMH = FM / AH;
+    static_assert(FM % AH == 0, "A fragment halves");
+    // POOL: the fragment addresses rebuilt per step from an opaque lane id (hoisted out of the
+    // loop they are a dozen more live VGPRs)
+    int ln = lane;
+    if constexpr (POOL) asm volatile("" : "+v"(ln));
+    const int c0 = 2 * (ln >> 4);
+    auto load_a = [&](int i) {
+      const int row = wm * TM + i * 16 + (ln & 15);
       const i32x4 lo = *reinterpret_cast<const i32x4*>(A + row * RB + ((c0 ^ swz8(row)) << 4));
       const i32x4 hi = *reinterpret_cast<const i32x4*>(A + row * RB + (((c0 + 1) ^ swz8(row)) << 4));
-      af[i] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
+      return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    };
+    i32x8 af[FMH], bfr[FN];
+#pragma unroll
+    for (int i = 0; i < FMH; ++i) af[i] = load_a(i);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int row = wn * TN + j * 16 + (lane & 15);
+      const int row = wn * TN + j * 16 + (ln & 15);
       const i32x4 lo = *reinterpret_cast<const i32x4*>(B + row * RB + ((c0 ^ swz8(row)) << 4));
       const i32x4 hi = *reinterpret_cast<const i32x4*>(B + row * RB + (((c0 + 1) ^ swz8(row)) << 4));
       bfr[j] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+    for (int h = 0; h < AH; ++h) {
+      if (h > 0) {
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+        for (int i = 0; i < FMH; ++i) af[i] = load_a(FMH * h + i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int i = 0; i < FMH; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[FMH * h + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[FMH * h + i][j], 0,
+                                                                                0, 0, 127, 0, 127);
+    }
     __builtin_amdgcn_sched_barrier(0);
     // slot (t + 1) & 1 held step t - 1, which every wave finished before this step's barrier
     if constexpr (POOL)
