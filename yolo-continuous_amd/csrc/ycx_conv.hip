@@ -2471,8 +2471,15 @@ __device__ __forceinline__ void wait_vm_counted(int nb) {
   }
 }
 
-template <int WCO, int WPX, int TPW, int KC, int NS, int SUB>
+// PIPE (KC <= 4, where 32 more accumulator VGPRs fit): a tile's epilogue (bias, activation,
+// bf16 pack) runs in the first K step of the next tile, beside that step's MFMAs (the
+// activation is a template argument so the two share one basic block and the scheduler can
+// interleave them), and its stores follow that step's MFMAs. In tile order the eight waves'
+// epilogues otherwise ran together with no MFMA on the CU (10-15 % of the launch at
+// cout >= 256, tests/probes/conv_bench.py CONV_ACT=0 against 1).
+template <int WCO, int WPX, int TPW, int KC, int NS, int SUB, int ACT>
 __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
+  constexpr bool PIPE = KC <= 4;
   constexpr int NW = WCO * WPX, PT = TPW * WPX, FM = 2, FN = TPW / 16, BCO = WCO * 32;
   constexpr int KS = KC / SUB, SLAB = PT * 128, STAGE = SUB * SLAB, A_PW = PT / (8 * NW);
   constexpr int NSTO = FN;  // 16-byte stores per wave per tile (A rows permuted: 8 channels per lane)
@@ -2536,19 +2543,45 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
 
   const bool exact = a.Cout == a.Cout_pad;  // then every full tile stores exactly NSTO times per wave
   elt_t* __restrict__ Y = reinterpret_cast<elt_t*>(a.y) + a.out_coff;
+  const float nl2e = silu_nl2e();  // act4_t: the packed form of ycx_act<true>, bit-identical
+  const int co = cob + 8 * (lane >> 4);  // channels co .. co+7 (cout % 8 == 0: all valid or none)
+  // tile tl's outputs from its sums: 8 channels of one pixel per lane and fragment column
+  auto finish = [&](const f32x4 (&s)[FM][FN], eltx8 (&ov)[FN]) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const f32x4 v = act4_t<ACT>(s[i][j] + bv[i], a.slope, nl2e);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ov[j][4 * i + q] = (elt_t)v[q];
+      }
+  };
+  auto store = [&](int tl, const eltx8 (&ov)[FN]) {
+    const int pb = (t0 + tl) * PT + wp * TPW + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int p = pb + 16 * j;
+      if (p < a.M && co < a.Cout) if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov[j];
+    }
+  };
+  f32x4 acc[FM][FN], accp[FM][FN];  // accp (PIPE): the previous tile's sums
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   int t = 0;
   for (int tl = 0; tl < t1 - t0; ++tl) {
-    f32x4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks, ++t) {
-      // wait for stage t: younger than its loads are the NS-2 later stages and
-      // the store batches of the tiles that ended in steps t-NS+1 .. t-1
+      // wait for stage t: younger than its loads are the NS-2 later stages and the store
+      // batches issued in steps t-NS+1 .. t-1 (a tile's batch: in its last step, or with PIPE
+      // in the next tile's first step)
       if (t + NS - 2 >= nst) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      } else if constexpr (PIPE) {
+        const int lo = t - NS + 1 > KS ? t - NS + 1 : KS;  // batches: steps i KS, i >= 1
+        const int nb = exact && t - 1 >= lo ? (t - 1) / KS - (lo + KS - 1) / KS + 1 : 0;
+        wait_vm_counted<VM_RING, 0, (NS + KS - 2) / KS * NSTO>(nb > 0 ? nb * NSTO : 0);
       } else {
         const int lo = t - NS + 1 > 0 ? t - NS + 1 : 0;  // tile ends: steps i KS + KS - 1
         const int nb = exact && t >= KS ? (t - 1 - (KS - 1)) / KS - (lo + KS - 1 - (KS - 1)) / KS + 1 : 0;
@@ -2557,6 +2590,15 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (t + NS - 1 < nst) issue(t + NS - 1);
+      if (ks == 0) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            if constexpr (PIPE) accp[i][j] = acc[i][j];
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      }
       const char* B = smem + (t % NS) * STAGE;
 #pragma unroll
       for (int kk = 0; kk < 2 * SUB; ++kk) {
@@ -2574,24 +2616,32 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres(ConvArgs a) {
           for (int j = 0; j < FN; ++j)
             acc[i][j] = YCX_MFMA16(af[2 * SUB * ks + kk][i], bfr[j], acc[i][j], 0, 0, 0);
       }
+      if constexpr (PIPE) {
+        if (ks == 0) {  // the previous tile's epilogue beside this step's MFMAs (same basic block)
+          eltx8 ov[FN];
+          finish(accp, ov);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {  // pinned here: otherwise sunk into the conditional stores below
+            const int4 w = __builtin_bit_cast(int4, ov[j]);
+            asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (tl > 0) store(tl - 1, ov);
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // epilogue from registers: no global loads here (one would make the compiler drain vmcnt)
-    const int pb = (t0 + tl) * PT + wp * TPW + (lane & 15);
-    const int co = cob + 8 * (lane >> 4);  // channels co .. co+7 (cout % 8 == 0: all valid or none)
-    const float nl2e = silu_nl2e();  // act4: the packed form of ycx_act<true>, bit-identical
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      eltx8 ov;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const f32x4 v = act4(acc[i][j] + bv[i], a.act, a.slope, nl2e);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)v[q];
-      }
-      const int p = pb + 16 * j;
-      if (p < a.M && co < a.Cout) if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov;
+    if constexpr (!PIPE) {
+      // epilogue from registers: no global loads here (one would make the compiler drain vmcnt)
+      eltx8 ov[FN];
+      finish(acc, ov);
+      store(tl, ov);
     }
+  }
+  if constexpr (PIPE) {
+    eltx8 ov[FN];
+    finish(acc, ov);
+    store(t1 - t0 - 1, ov);
   }
 }
 
@@ -3287,6 +3337,18 @@ ycx_status launch_f8(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
+template <int WCO, int WPX, int TPW, int NS, int SUB, int ACT>
+ycx_status launch_wres_cin(const ConvArgs& a, dim3 g, dim3 b, hipStream_t st) {
+  switch (a.Cin) {
+    case 64: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 1, NS, 1, ACT>), g, b, 0, st, a); break;
+    case 128: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 2, NS, SUB, ACT>), g, b, 0, st, a); break;
+    case 256: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 4, NS, SUB, ACT>), g, b, 0, st, a); break;
+    case 512: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 8, NS, SUB, ACT>), g, b, 0, st, a); break;
+    default: return YCX_ERR_UNSUPPORTED;
+  }
+  return ycx_launch_status();
+}
+
 // Weight-resident 1x1 (tile 22): the wave split follows cout_pad, the K unroll Cin.
 template <int WCO, int WPX, int TPW, int NS, int SUB>
 ycx_status launch_wres_k(ConvArgs a, hipStream_t st) {
@@ -3295,14 +3357,11 @@ ycx_status launch_wres_k(ConvArgs a, hipStream_t st) {
   const int R = std::max(1, std::min(T, 256 / a.n_ct));
   a.nwg = R * a.n_ct;
   dim3 g(a.nwg), b(WCO * WPX * 64);
-  switch (a.Cin) {
-    case 64: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 1, NS, 1>), g, b, 0, st, a); break;
-    case 128: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 2, NS, SUB>), g, b, 0, st, a); break;
-    case 256: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 4, NS, SUB>), g, b, 0, st, a); break;
-    case 512: hipLaunchKernelGGL((conv1x1_wres<WCO, WPX, TPW, 8, NS, SUB>), g, b, 0, st, a); break;
-    default: return YCX_ERR_UNSUPPORTED;
+  switch (a.act) {
+    case YCX_ACT_SILU: return launch_wres_cin<WCO, WPX, TPW, NS, SUB, YCX_ACT_SILU>(a, g, b, st);
+    case YCX_ACT_LEAKY: return launch_wres_cin<WCO, WPX, TPW, NS, SUB, YCX_ACT_LEAKY>(a, g, b, st);
+    default: return launch_wres_cin<WCO, WPX, TPW, NS, SUB, YCX_ACT_NONE>(a, g, b, st);
   }
-  return ycx_launch_status();
 }
 
 bool wres_ok(const ConvArgs& a) {
