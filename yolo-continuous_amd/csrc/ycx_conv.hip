@@ -2848,7 +2848,8 @@ __global__ void __launch_bounds__(512) conv1x1_wres_pair(ConvArgs a, ConvArgs b)
 // exactly FM x FN dword stores per wave, counted into the next waits.
 // Requires 1x1/s1/p0, cin = 128 KC (KC = 1, 2, 4), NHWC e4m3 output without residual.
 // -------------------------------------------------------------------------
-template <int WCO, int WPX, int TPW, int KC, int NS>
+// The epilogue runs beside the next tile's first-step MFMAs as in conv1x1_wres (PIPE there).
+template <int WCO, int WPX, int TPW, int KC, int NS, int ACT>
 __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
   constexpr int NW = WCO * WPX, PT = TPW * WPX, FM = 2, FN = TPW / 16, BCO = WCO * 32;
   constexpr int STAGE = PT * 128, A_PW = PT / (8 * NW);
@@ -2916,27 +2917,56 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
   const bool exact = a.Cout == a.Cout_pad;  // then every full tile stores exactly NSTO times per wave
   uint8_t* __restrict__ Y = reinterpret_cast<uint8_t*>(a.y) + a.out_coff;
   const float osc = a.out_scale;
+  const float nl2e = silu_nl2e();  // act4_t and a packed fma: bit-identical to fmaf + ycx_act<true>
+  const int co = cob + 8 * (lane >> 4);  // channels co .. co+7 (cout % 8 == 0: all valid or none)
+  auto finish = [&](const f32x4 (&s)[FM][FN], uint2 (&ov)[FN]) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      f32x4 x[FM];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) x[i] = act4_t<ACT>(__builtin_elementwise_fma(s[i][j], qv[i], bv[i]), a.slope, nl2e) * osc;
+      ov[j] = make_uint2(f8x4_pack(x[0][0], x[0][1], x[0][2], x[0][3]), f8x4_pack(x[1][0], x[1][1], x[1][2], x[1][3]));
+    }
+  };
+  auto store = [&](int tl, const uint2 (&ov)[FN]) {
+    const int pb = (t0 + tl) * PT + wp * TPW + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int p = pb + 16 * j;
+      if (p < a.M && co < a.Cout) if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(uint2))) *reinterpret_cast<uint2*>(Y + (size_t)p * a.out_cs + co) = ov[j];
+    }
+  };
+  static_assert(FM == 2, "two fragments: 8 channels per lane");
+  f32x4 acc[FM][FN], accp[FM][FN];  // accp: the previous tile's sums
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   int t = 0;
   for (int tl = 0; tl < t1 - t0; ++tl) {
-    f32x4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KC; ++ks, ++t) {
-      // wait for stage t: younger than its loads are the NS-2 later stages and
-      // the store batches of the tiles that ended in steps t-NS+1 .. t-1
+      // wait for stage t: younger than its loads are the NS-2 later stages and the store
+      // batches issued in steps t-NS+1 .. t-1 (a tile's batch in the next tile's first step)
       if (t + NS - 2 >= nst) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       } else {
-        const int lo = t - NS + 1 > 0 ? t - NS + 1 : 0;  // tile ends: steps i KC + KC - 1
-        const int nb = exact && t >= KC ? (t - 1 - (KC - 1)) / KC - (lo + KC - 1 - (KC - 1)) / KC + 1 : 0;
-        wait_vm_counted<VM_RING, 0, (NS + KC - 2) / KC * NSTO>(nb * NSTO);
+        const int lo = t - NS + 1 > KC ? t - NS + 1 : KC;  // batches: steps i KC, i >= 1
+        const int nb = exact && t - 1 >= lo ? (t - 1) / KC - (lo + KC - 1) / KC + 1 : 0;
+        wait_vm_counted<VM_RING, 0, (NS + KC - 2) / KC * NSTO>(nb > 0 ? nb * NSTO : 0);
       }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (t + NS - 1 < nst) issue(t + NS - 1);
+      if (ks == 0) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            accp[i][j] = acc[i][j];
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      }
       const char* B = smem + (t % NS) * STAGE;
       i32x8 bfr[FN];
 #pragma unroll
@@ -2952,25 +2982,21 @@ __global__ void __launch_bounds__(WCO * WPX * 64) conv1x1_wres_f8(ConvArgs a) {
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[ks][i], bfr[j], acc[i][j], 0, 0, 0, 127,
                                                                        0, 127);
+      if (ks == 0) {  // the previous tile's epilogue beside this step's MFMAs (same basic block)
+        uint2 ov[FN];
+        finish(accp, ov);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(ov[j].x), "v"(ov[j].y));  // not sunk into the stores
+        __builtin_amdgcn_sched_barrier(0);
+        if (tl > 0) store(tl - 1, ov);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // epilogue from registers: no global loads here (one would make the compiler drain vmcnt)
-    const int pb = (t0 + tl) * PT + wp * TPW + (lane & 15);
-    const int co = cob + 8 * (lane >> 4);  // channels co .. co+7 (cout % 8 == 0: all valid or none)
-    const float nl2e = silu_nl2e();  // act4 and a packed fma: bit-identical to fmaf + ycx_act<true>
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float v[8];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const f32x4 x = act4(__builtin_elementwise_fma(acc[i][j], qv[i], bv[i]), a.act, a.slope, nl2e) * osc;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[4 * i + q] = x[q];
-      }
-      const uint2 ov = make_uint2(f8x4_pack(v[0], v[1], v[2], v[3]), f8x4_pack(v[4], v[5], v[6], v[7]));
-      const int p = pb + 16 * j;
-      if (p < a.M && co < a.Cout) if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(uint2))) *reinterpret_cast<uint2*>(Y + (size_t)p * a.out_cs + co) = ov;
-    }
+  }
+  {
+    uint2 ov[FN];
+    finish(acc, ov);
+    store(t1 - t0 - 1, ov);
   }
 }
 
@@ -3414,6 +3440,17 @@ bool wres_f8_ok(const ConvArgs& a) {
          (long long)a.M * a.in_cs < (1LL << 31) - 64;
 }
 
+template <int WCO, int WPX, int TPW, int NS, int ACT>
+ycx_status launch_wres_f8_cin(const ConvArgs& a, dim3 g, dim3 b, hipStream_t st) {
+  switch (a.Cin) {
+    case 128: hipLaunchKernelGGL((conv1x1_wres_f8<WCO, WPX, TPW, 1, NS, ACT>), g, b, 0, st, a); break;
+    case 256: hipLaunchKernelGGL((conv1x1_wres_f8<WCO, WPX, TPW, 2, NS, ACT>), g, b, 0, st, a); break;
+    case 512: hipLaunchKernelGGL((conv1x1_wres_f8<WCO, WPX, TPW, 4, NS, ACT>), g, b, 0, st, a); break;
+    default: return YCX_ERR_UNSUPPORTED;
+  }
+  return ycx_launch_status();
+}
+
 template <int WCO, int WPX, int TPW, int NS>
 ycx_status launch_wres_f8_k(ConvArgs a, hipStream_t st) {
   a.n_ct = a.Cout_pad / (WCO * 32);
@@ -3421,13 +3458,11 @@ ycx_status launch_wres_f8_k(ConvArgs a, hipStream_t st) {
   const int R = std::max(1, std::min(T, 256 / a.n_ct));
   a.nwg = R * a.n_ct;
   dim3 g(a.nwg), b(WCO * WPX * 64);
-  switch (a.Cin) {
-    case 128: hipLaunchKernelGGL((conv1x1_wres_f8<WCO, WPX, TPW, 1, NS>), g, b, 0, st, a); break;
-    case 256: hipLaunchKernelGGL((conv1x1_wres_f8<WCO, WPX, TPW, 2, NS>), g, b, 0, st, a); break;
-    case 512: hipLaunchKernelGGL((conv1x1_wres_f8<WCO, WPX, TPW, 4, NS>), g, b, 0, st, a); break;
-    default: return YCX_ERR_UNSUPPORTED;
+  switch (a.act) {
+    case YCX_ACT_SILU: return launch_wres_f8_cin<WCO, WPX, TPW, NS, YCX_ACT_SILU>(a, g, b, st);
+    case YCX_ACT_LEAKY: return launch_wres_f8_cin<WCO, WPX, TPW, NS, YCX_ACT_LEAKY>(a, g, b, st);
+    default: return launch_wres_f8_cin<WCO, WPX, TPW, NS, YCX_ACT_NONE>(a, g, b, st);
   }
-  return ycx_launch_status();
 }
 
 // tile 37: fp8 weight-stationary 3x3 64 -> 64, one persistent block per CU
