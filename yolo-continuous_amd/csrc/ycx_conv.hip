@@ -1716,12 +1716,43 @@ __global__ void __launch_bounds__(512) conv3x3s2_wsr(ConvArgs a) {
   for (int q = 1; q < NB - 1; ++q)
     if (tb + q < te) issue_h(tb + q, q);
 
+  // a tile's epilogue runs beside the next tile's MFMAs (as conv1x1_wres's PIPE): accp holds the
+  // previous tile's sums, its stores follow this tile's MFMAs
+  f32x4 accp[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) accp[i][j] = bv[i];
+  const int co = 32 * wm + 8 * (lane >> 4);
+  auto finish = [&](const f32x4 (&s)[FM][FN], eltx8 (&ov)[FN]) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const f32x4 x = act4_t<ACT>(s[i][j], a.slope, nl2e);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ov[j][4 * i + q] = (elt_t)x[q];
+      }
+  };
+  auto store = [&](int tile, const eltx8 (&ov)[FN]) {
+    const int n = tile / tpi, ti = tile - n * tpi;
+    const int oy0 = (ti / tx_n) * TH, ox0 = (ti % tx_n) * TW;
+    if (co < a.Cout) {  // cout % 8 == 0: the 8 channels are all valid
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int p = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0 + (lane & 15);
+        if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov[j];
+      }
+    }
+  };
   for (int tile = tb; tile < te; ++tile) {
     const int k = tile - tb, b = k % NB;
     // in flight behind this tile's halo: the halos of the next min(NB - 2, te - 1 - tile) tiles,
-    // then (exact, k > 0) the previous tile's FN stores; the weights came before them
+    // then (exact) the FN stores of tiles max(0, k - NB) .. k - 2 (tile j's go out in tile j + 1,
+    // after the halo of j + NB); the weights came before them
     const int ahead = min(NB - 2, te - 1 - tile);
-    vm_wait_le<(NB - 2) * HPW + FN>(ahead * nh + (k > 0 && exact ? FN : 0));
+    const int nsb = exact ? max(0, k - 1 - max(0, k - NB)) : 0;
+    vm_wait_le<(NB - 2) * HPW + (NB - 1) * FN>(ahead * nh + nsb * FN);
     __syncthreads();  // this tile's halo landed; every wave is done with the previous tile's buffer
     if (tile + NB - 1 < te) issue_h(tile + NB - 1, (k + NB - 1) % NB);
     const char* halo = smem + b * HBUF;
@@ -1752,24 +1783,25 @@ __global__ void __launch_bounds__(512) conv3x3s2_wsr(ConvArgs a) {
           for (int j = 0; j < FN; ++j) acc[i][j] = YCX_MFMA16(wf[t][kk][i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
-    const int n = tile / tpi, ti = tile - n * tpi;
-    const int oy0 = (ti / tx_n) * TH, ox0 = (ti % tx_n) * TW;
-    const int co = 32 * wm + 8 * (lane >> 4);
-    if (co < a.Cout) {  // cout % 8 == 0: the 8 channels are all valid
+    {  // the previous tile's epilogue beside this tile's MFMAs (one basic block)
+      eltx8 ov[FN];
+      finish(accp, ov);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int p = n * a.HoWo + (oy0 + wn * FN + j) * a.Wo + ox0 + (lane & 15);
-        eltx8 ov;
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const f32x4 x = act4_t<ACT>(acc[i][j], a.slope, nl2e);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) ov[4 * i + q] = (elt_t)x[q];
-        }
-        if (YCX_OUT_OK(a, Y + (size_t)p * a.out_cs + co, sizeof(eltx8))) *reinterpret_cast<eltx8*>(Y + (size_t)p * a.out_cs + co) = ov;
+      for (int j = 0; j < FN; ++j) {  // pinned here: otherwise sunk into the conditional stores below
+        const int4 w = __builtin_bit_cast(int4, ov[j]);
+        asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));
       }
+      __builtin_amdgcn_sched_barrier(0);
+      if (k > 0) store(tile - 1, ov);
     }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) accp[i][j] = acc[i][j];
   }
+  eltx8 ov[FN];
+  finish(accp, ov);
+  store(te - 1, ov);
 }
 
 // TH x TW output tiles. TW = 16: a fragment is one tile row. Band mode (TW != 16, r03): TW is
