@@ -703,7 +703,8 @@ __device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const fl
 // weight DMA of t + 1 and four 16-byte global loads per pixel row (the 2x2 window),
 // and after step t's MFMAs takes their max and writes it to the LDS slot where the
 // activation DMA would have put it. The pooled map never reaches HBM.
-template <int BM, int BN, int WM, int WN, bool TT, int NST, int NSB = NST, bool HEAD = false, bool POOL = false>
+template <int BM, int BN, int WM, int WN, bool TT, int NST, int NSB = NST, bool HEAD = false, bool POOL = false,
+          bool KCM = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadArgs hd) {
   constexpr int NW = WM * WN;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
@@ -787,7 +788,10 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   // steps after its first read at Cin 128 (up to 48 at Cin 512), long enough for the concurrent
   // tiles of an XCD to evict it from the 4 MB L2: 1.9-2.5x the input bytes came from beyond the
   // L2 (tests/probes/pmc_s2.sh). Step s is chunk s / 9, tap kTapS2[s % 9]; A follows the same K.
-  const bool kcm = !TT && !POOL && a.S == 2 && a.KH == 3 && a.KW == 3 && a.Cin == 128;
+  // A template instance (KCM, launched for 3x3/s2 at Cin 128 only): as a runtime test it cost
+  // every tile-16 launch up to 8 % (the uniform branches in both issue paths).
+  constexpr bool kcm = KCM;
+  static_assert(!KCM || (!TT && !POOL && !HEAD), "K order for plain 3x3/s2 steps");
   constexpr unsigned long long kTapS2 = 0x453786201ull;  // 4 bits per position: taps 0 2 1 6 8 7 3 5 4
   auto k_of = [&](int s) {  // K element offset of step s in the packed weight row
     if (!kcm) return s * BK;
@@ -3345,6 +3349,19 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
     }
   }
   if (a.pool) return YCX_ERR_UNSUPPORTED;
+  if constexpr (!TT && NST == 2 && NSB == 2 && BM == 128 && BN == 128) {  // tile 16 on a 3x3/s2 at Cin 128
+#if defined(YCX_KCM_ALL)  // development A/B: every Cin
+    if (a.S == 2 && a.KH == 3 && a.KW == 3) {
+#elif !defined(YCX_NO_KCM)  // YCX_NO_KCM: the (tap, chunk) order on these too
+    if (a.S == 2 && a.KH == 3 && a.KW == 3 && a.Cin == 128) {
+#else
+    if (false) {
+#endif
+      hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, false, 2, 2, false, false, true>), dim3(a.nwg),
+                         dim3(WM * WN * 64), 0, st, a, HeadArgs{});
+      return ycx_launch_status();
+    }
+  }
   hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, TT, NST, NSB>), dim3(a.nwg), dim3(WM * WN * 64), 0, st, a,
                      HeadArgs{});
   return ycx_launch_status();
