@@ -146,6 +146,9 @@ CASES = [  # n, h, w, cin, cout, k, s, act, extras
     (1, 33, 17, 128, 64, 1, 1, L.ACT_LEAKY, {}),
     (2, 16, 16, 256, 128, 1, 1, L.ACT_SILU, dict(in_extra=128, out_extra=64)),
     (3, 20, 20, 256, 200, 1, 1, L.ACT_SILU, {}),     # cout < cout_pad
+    (2, 96, 96, 256, 256, 1, 1, L.ACT_SILU, {}),     # several tiles per block: deferred epilogues
+    (3, 70, 70, 512, 128, 1, 1, L.ACT_SILU, {}),
+    (2, 90, 90, 128, 64, 1, 1, L.ACT_NONE, {}),
     (2, 32, 32, 64, 64, 3, 1, L.ACT_SILU, {}),       # weight-stationary 3x3 64 -> 64 (tile 37) cases
     (1, 16, 48, 64, 48, 3, 1, L.ACT_LEAKY, {}),
     (2, 32, 16, 64, 64, 3, 1, L.ACT_NONE, dict(in_extra=64, out_extra=64)),

@@ -137,12 +137,25 @@ def test_conv1x1_wres(device, cin, cout):
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize('act', [L.ACT_LEAKY, L.ACT_SILU, L.ACT_NONE])
 @pytest.mark.parametrize('n,hw,cin,cout', [(2, 128, 256, 256), (1, 128, 256, 512), (4, 128, 128, 128),
-                                           (2, 96, 64, 64), (3, 72, 512, 256)])
-def test_conv1x1_wres_multi_tile(device, n, hw, cin, cout):
+                                           (2, 96, 64, 64), (3, 72, 512, 256), (3, 70, 256, 248)])
+def test_conv1x1_wres_multi_tile(device, n, hw, cin, cout, act):
     """Several tiles per persistent block: the LDS ring wraps across tile
-    boundaries with the epilogue stores counted into the next waits."""
-    got, ref = _run_conv(device, n, hw, hw, cin, cout, 1, 1, L.ACT_LEAKY, 22, L.DT_BF16, in_extra=8, out_extra=8)
+    boundaries with the epilogue stores counted into the next waits; at cin <= 256 each
+    tile's epilogue runs in the next tile's first K step (one instance per activation), the
+    last one after the loop; a ragged last tile and cout < cout_pad (uncounted stores)."""
+    got, ref = _run_conv(device, n, hw, hw, cin, cout, 1, 1, act, 22, L.DT_BF16, in_extra=8, out_extra=8)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize('n,hw,cout,act', [(2, (40, 40), 128, L.ACT_SILU), (1, (33, 47), 120, L.ACT_LEAKY),
+                                           (3, (64, 48), 256, L.ACT_NONE), (2, (160, 160), 128, L.ACT_SILU)])
+def test_tile16_s2_cin128_chunk_major(device, n, hw, cout, act):
+    """Tile 16 on a 3x3/s2 conv at cin 128 walks K channel-chunk-major with paired taps (its
+    KCM template instance): odd map sizes (taps outside the image), several pixel and channel
+    tiles, cout < cout_pad, channel-sliced input/output."""
+    got, ref = _run_conv(device, n, hw[0], hw[1], 128, cout, 3, 2, act, 16, L.DT_BF16, in_extra=8, out_extra=16)
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
 
 

@@ -3350,13 +3350,7 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
   }
   if (a.pool) return YCX_ERR_UNSUPPORTED;
   if constexpr (!TT && NST == 2 && NSB == 2 && BM == 128 && BN == 128) {  // tile 16 on a 3x3/s2 at Cin 128
-#if defined(YCX_KCM_ALL)  // development A/B: every Cin
-    if (a.S == 2 && a.KH == 3 && a.KW == 3) {
-#elif !defined(YCX_NO_KCM)  // YCX_NO_KCM: the (tap, chunk) order on these too
-    if (a.S == 2 && a.KH == 3 && a.KW == 3 && a.Cin == 128) {
-#else
-    if (false) {
-#endif
+    if (a.S == 2 && a.KH == 3 && a.KW == 3 && a.Cin == 128) {  // Cin 256 / 512: slower
       hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, false, 2, 2, false, false, true>), dim3(a.nwg),
                          dim3(WM * WN * 64), 0, st, a, HeadArgs{});
       return ycx_launch_status();
