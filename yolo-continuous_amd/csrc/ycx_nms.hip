@@ -107,7 +107,7 @@ constexpr int kPrepClsB = YCX_PREP_CLS_B;
 constexpr int kSplitTasks = YCX_NMS_SPLIT_TASKS;
 
 struct Layout {
-  size_t hdr, tasks, wframes, wcells, fframes, fcells, bcnt, per_image_base;  // header + task tables +
+  size_t hdr, tasks, wframes, wcells, fframes, fcells, bcnt, bits, per_image_base;  // header + task tables +
                                   // wide / split-fast class indexes + slice class counts (batch), then per image:
   size_t keys, bucket, kept, sbox, srank, nsup, slots, state, cnt, offs, kc, per_image;
   int max_tasks, max_wide;  // big classes per image; wide classes per image
@@ -138,7 +138,8 @@ __host__ __device__ inline Layout layout(int n, int rows) {
   L.fframes = al(L.wcells + (size_t)n * L.max_wide * wide_cells_bytes());
   L.fcells = al(L.fframes + (size_t)kSplitTasks * wframe_bytes());
   L.bcnt = al(L.fcells + (size_t)kSplitTasks * fast_cells_bytes());
-  L.per_image_base = al(L.bcnt + (size_t)n * kPrepB * kMaxNc * 4);
+  L.bits = al(L.bcnt + (size_t)n * kPrepB * kMaxNc * 4);  // per image: a candidate flag byte per row
+  L.per_image_base = al(L.bits + (size_t)n * rows);
   size_t o = 0;
   // keys: a class at bucket offset `off` with S rows sorts at keys + 2*off; its
   // power-of-two span is < 2S and off + S <= rows, so 2*rows keys suffice.
@@ -355,6 +356,28 @@ __device__ __forceinline__ void prep_slice(int cnt, int b, int& i0, int& i1) {
   i1 = (int)((long long)cnt * (b + 1) / kPrepB);
 }
 
+// nms_mark sets the flag byte of every listed candidate's row (the list is in append order; plain
+// byte stores: 32 candidates per u32 word made atomicOr on a bitmap 42 us at C2); nms_count /
+// nms_bucket then walk rows in ascending order, slice b = rows [r0, r1), so every class bucket
+// lists its rows in ascending order (a stable counting sort by class). The score sorts downstream are stable LSD passes over the score
+// digits only: equal scores keep that row order, which is the reference's (score desc, row asc).
+__global__ void __launch_bounds__(kThreads) nms_mark(ycx_nms_desc d, const int* __restrict__ cand_rows,
+                                                     const int* __restrict__ cand_counts, char* ws) {
+  const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  const int rows = d.rows_total;
+  const Layout L = layout(d.n, rows);
+  unsigned char* flag = reinterpret_cast<unsigned char*>(ws + L.bits) + (size_t)img * rows;
+  const int* cr = cand_rows + (size_t)img * rows;
+  int i0, i1;
+  prep_slice(min(cand_counts[img], rows), b, i0, i1);
+  for (int i = i0 + tid; i < i1; i += kThreads) flag[cr[i]] = 1;
+}
+
+__device__ __forceinline__ void row_slice(int rows, int b, int& r0, int& r1) {
+  r0 = (int)((long long)rows * b / kPrepB);
+  r1 = (int)((long long)rows * (b + 1) / kPrepB);
+}
+
 __global__ void __launch_bounds__(kThreads) nms_count(ycx_nms_desc d, const ycx_cand* __restrict__ cand,
                                                       const int* __restrict__ cand_rows,
                                                       const int* __restrict__ cand_counts, char* ws) {
@@ -363,12 +386,13 @@ __global__ void __launch_bounds__(kThreads) nms_count(ycx_nms_desc d, const ycx_
   const int nc = d.nc, rows = d.rows_total;
   const Layout L = layout(d.n, rows);
   const ycx_cand* ci = cand + (size_t)img * rows;
-  const int* cr = cand_rows + (size_t)img * rows;
-  int i0, i1;
-  prep_slice(min(cand_counts[img], rows), b, i0, i1);
+  const unsigned char* flag = reinterpret_cast<const unsigned char*>(ws + L.bits) + (size_t)img * rows;
+  int r0, r1;
+  row_slice(rows, b, r0, r1);
   for (int c = tid; c < nc; c += kThreads) s_cnt[c] = 0;
   __syncthreads();
-  for (int i = i0 + tid; i < i1; i += kThreads) atomicAdd(&s_cnt[ci[cr[i]].cls], 1);
+  for (int r = r0 + tid; r < r1; r += kThreads)
+    if (flag[r]) atomicAdd(&s_cnt[ci[r].cls], 1);
   __syncthreads();
   int* bc = reinterpret_cast<int*>(ws + L.bcnt) + ((size_t)img * kPrepB + b) * kMaxNc;
   for (int c = tid; c < nc; c += kThreads) bc[c] = s_cnt[c];
@@ -377,13 +401,15 @@ __global__ void __launch_bounds__(kThreads) nms_count(ycx_nms_desc d, const ycx_
 __global__ void __launch_bounds__(kThreads) nms_bucket(ycx_nms_desc d, const ycx_cand* __restrict__ cand,
                                                        const int* __restrict__ cand_rows,
                                                        const int* __restrict__ cand_counts, char* ws) {
-  __shared__ int s_cnt[kMaxNc], s_off[kMaxNc], s_base[kMaxNc], s_fill[kMaxNc];
-  const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, wid = tid >> 6;
+  constexpr int NW = kThreads / 64;
+  __shared__ int s_cnt[kMaxNc], s_off[kMaxNc], s_base[kMaxNc];
+  __shared__ unsigned short s_wc[NW][kMaxNc];  // per (wave, class) rows of the current chunk
+  const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int nc = d.nc, rows = d.rows_total;
   const Layout L = layout(d.n, rows);
   const Ptrs P = image_ptrs(ws, L, img);
   const ycx_cand* ci = cand + (size_t)img * rows;
-  const int* cr = cand_rows + (size_t)img * rows;
+  const unsigned char* flag = reinterpret_cast<const unsigned char*>(ws + L.bits) + (size_t)img * rows;
   const int* bc = reinterpret_cast<const int*>(ws + L.bcnt) + (size_t)img * kPrepB * kMaxNc;
   for (int c = tid; c < nc; c += kThreads) {
     int tot = 0, before = 0;
@@ -394,8 +420,8 @@ __global__ void __launch_bounds__(kThreads) nms_bucket(ycx_nms_desc d, const ycx
     }
     s_cnt[c] = tot;
     s_base[c] = before;
-    s_fill[c] = 0;
   }
+  for (int k = tid; k < NW * kMaxNc; k += kThreads) (&s_wc[0][0])[k] = 0;
   __syncthreads();
   if (wid == 0) wave_exclusive_scan(s_cnt, s_off, nc);
   __syncthreads();
@@ -404,12 +430,41 @@ __global__ void __launch_bounds__(kThreads) nms_bucket(ycx_nms_desc d, const ycx
       P.cnt[c] = s_cnt[c];
       P.offs[c] = s_off[c];
     }
-  int i0, i1;
-  prep_slice(min(cand_counts[img], rows), b, i0, i1);
-  for (int i = i0 + tid; i < i1; i += kThreads) {
-    const int r = cr[i];
-    const int c = ci[r].cls;
-    P.bucket[s_off[c] + s_base[c] + atomicAdd(&s_fill[c], 1)] = r;
+  // rows of the slice in chunks of kThreads, thread t <-> row r0 + t: a class's rows go to its
+  // bucket in row order (rank among the chunk's earlier rows of the class: earlier waves' counts
+  // plus the lanes below in this wave; s_base carries the earlier chunks)
+  int rb, r_end;
+  row_slice(rows, b, rb, r_end);
+  int nbits = 0;
+  while ((1 << nbits) <= nc) ++nbits;  // class + 1 in [0, nc]: 0 = no candidate
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int r0 = rb; r0 < r_end; r0 += kThreads) {  // uniform trip count
+    const int r = r0 + tid;
+    const bool valid = r < r_end && flag[r];
+    const int c1 = valid ? ci[r].cls + 1 : 0;
+    unsigned long long m = ~0ull;
+    for (int bit = 0; bit < nbits; ++bit) {
+      const unsigned long long bl = __ballot((c1 >> bit) & 1);
+      m &= ((c1 >> bit) & 1) ? bl : ~bl;
+    }
+    if (valid && (m & lt) == 0) s_wc[wid][c1 - 1] = (unsigned short)__popcll(m);
+    __syncthreads();
+    if (valid) {
+      const int c = c1 - 1;
+      int q = s_off[c] + s_base[c] + __popcll(m & lt);
+      for (int w = 0; w < wid; ++w) q += s_wc[w][c];
+      P.bucket[q] = r;
+    }
+    __syncthreads();
+    for (int c = tid; c < nc; c += kThreads) {
+      int add = 0;
+      for (int w = 0; w < NW; ++w) {
+        add += s_wc[w][c];
+        s_wc[w][c] = 0;
+      }
+      s_base[c] += add;
+    }
+    __syncthreads();
   }
 }
 
@@ -813,7 +868,9 @@ __device__ __forceinline__ void big_fast(const Task& tk, const ycx_cand* __restr
   // (2) rank sort in registers (exchange through LDS), then every element learns its rank
   unsigned long long* xch = reinterpret_cast<unsigned long long*>(smem);
   unsigned short* rank_of = reinterpret_cast<unsigned short*>(smem + 8 * kFastMax);
-  radix_sort_regs<E>(key, S, 13, xch, reinterpret_cast<unsigned short*>(smem + 10 * kFastMax), s_w, s_msk);
+  // bits [32, 64) only: the bucket lists the class's rows in ascending order and the passes are
+  // stable, so equal scores keep row order (the row digits were 4 of a C2 class's ~11 passes)
+  radix_sort_regs<E>(key, S, 32, xch, reinterpret_cast<unsigned short*>(smem + 10 * kFastMax), s_w, s_msk);
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < E; ++i)
@@ -1263,15 +1320,17 @@ __device__ void radix_rank(const ycx_cand* __restrict__ ci, int* bucket, int S, 
   }
   __syncthreads();
   const unsigned long long diff = s_msk[0] ^ s_msk[1];
-  int last = -1;  // the last digit any two keys differ in (none: S == 1, bucket already in order)
-  for (int sh = 0; sh < 64; sh += B)
+  // digits of the high word (the score) only: the bucket lists the class's rows in ascending
+  // order and the passes are stable, so equal scores keep row order (nms_bucket)
+  int last = -1;  // the last digit any two keys differ in (none: every score equal, bucket already in order)
+  for (int sh = 32; sh < 64; sh += B)
     if ((diff >> sh) & DM) last = sh;
   const int nC = D * E * NW;
 #ifdef YCX_NMS_PROFILE
   unsigned long long t_prev_ = __builtin_amdgcn_s_memtime();
   if (tid == 0) atomicAdd(&g_nms_wprof[8], t_prev_ - t_sort0);
 #endif
-  for (int sh = 0; sh <= last; sh += B) {
+  for (int sh = 32; sh <= last; sh += B) {
     if (((diff >> sh) & DM) == 0) continue;  // uniform
     for (int c = tid; c < nC; c += kBigThreads) C[c] = 0;
     __syncthreads();
@@ -2033,6 +2092,9 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   const int all_pairs = !(d->iou_thres >= 0.0);
   const float t_lo = all_pairs ? 0.0f : (float)(fmin(d->iou_thres, 1.0) * (1.0 - 1e-3));
   const float inv_t = t_lo > 0.0f ? 1.0f / t_lo : INFINITY;
+  if (hipMemsetAsync(ws + layout(d->n, d->rows_total).bits, 0, (size_t)d->n * d->rows_total, st) != hipSuccess)
+    return YCX_ERR_LAUNCH;  // the candidate flags
+  hipLaunchKernelGGL(nms_mark, dim3(kPrepB, d->n), dim3(kThreads), 0, st, *d, cand_rows, cand_counts, ws);
   hipLaunchKernelGGL(nms_count, dim3(kPrepB, d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws);
   hipLaunchKernelGGL(nms_bucket, dim3(kPrepB, d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws);
   hipLaunchKernelGGL(nms_prep, dim3(kPrepClsB, d->n), dim3(kThreads), 0, st, *d, cand, ws, t);
