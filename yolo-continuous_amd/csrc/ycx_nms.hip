@@ -1,9 +1,10 @@
 // Per-image, per-class greedy NMS with torchvision.ops.nms semantics -- the
 // loop of detect.py:124-137 (unique classes ascending, nms per class, results
-// concatenated class by class) for the whole batch in seven launches.
+// concatenated class by class) for the whole batch in eight launches.
 //
-//  nms_count / nms_bucket / nms_prep   16 workgroups per image: class histograms
-//              of candidate slices, exclusive scan -> one bucket per class; every
+//  nms_mark / nms_count / nms_bucket / nms_prep   16 workgroups per image: a flag
+//              byte per candidate row, class histograms of row slices, exclusive
+//              scan -> one bucket per class listing its rows in ascending order; every
 //              wave pulls whole classes from an LDS counter and a class of S <= 512
 //              candidates is finished entirely in registers (64*R keys
 //              bitonic-sorted across lanes and register slots, greedy scan with
