@@ -566,3 +566,17 @@ def test_nms_big_class_score_ties(device):
     _check_keep(wide, 1, 0.0, 0.3)
     wide[..., 4] = 0.75  # one score: the keys differ in the row bits only, the bin rank orders by row
     _check_keep(wide, 1, 0.0, 0.3)
+
+
+def test_nms_row_ordered_buckets_many_classes(device):
+    """The class bucketing walks row slices in ascending order with a per-wave class match (ten
+    ballots at nc = 600): every class bucket lists its rows in ascending order, so the score
+    sorts (score digits only) keep equal scores in row order. Hundreds of small classes, one
+    LDS-resident and one wide class with few distinct scores, a row count that splits unevenly
+    over the slices."""
+    pred = _random_pred(2, 30001, 600, seed=21, size_lo=-2.5, size_hi=-1.0)
+    g = torch.Generator().manual_seed(22)
+    pred[0, :7000, 5 + 17] = 2.0                                  # class 17 of image 0: ~7k rows
+    pred[1, 5:20005, 5 + 599] = 2.0                               # class 599 of image 1: 20k rows
+    pred[1, 5:20005, 4] = 0.5 + 0.0625 * torch.randint(0, 8, (20000,), generator=g).float()
+    _check_keep(pred, 600, 0.0, 0.45)
