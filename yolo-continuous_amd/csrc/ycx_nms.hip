@@ -1,10 +1,10 @@
 // Per-image, per-class greedy NMS with torchvision.ops.nms semantics -- the
 // loop of detect.py:124-137 (unique classes ascending, nms per class, results
-// concatenated class by class) for the whole batch in eight launches.
+// concatenated class by class) for the whole batch in seven launches.
 //
-//  nms_mark / nms_count / nms_bucket / nms_prep   16 workgroups per image: a flag
-//              byte per candidate row, class histograms of row slices, exclusive
-//              scan -> one bucket per class listing its rows in ascending order; every
+//  nms_mark / nms_bucket / nms_prep   16 workgroups per image: a flag byte per
+//              candidate row and class histograms of row slices, exclusive scan ->
+//              one bucket per class listing its rows in ascending order; every
 //              wave pulls whole classes from an LDS counter and a class of S <= 512
 //              candidates is finished entirely in registers (64*R keys
 //              bitonic-sorted across lanes and register slots, greedy scan with
@@ -89,7 +89,7 @@ struct Task {  // one large class
   int img, cls, off, S;
 };
 
-constexpr int kPrepB = 16;  // workgroups per image in the class bucketing (nms_count / nms_bucket)
+constexpr int kPrepB = 16;  // workgroups per image in the class bucketing (nms_mark / nms_bucket)
 #ifndef YCX_PREP_CLS_B
 #define YCX_PREP_CLS_B 4
 #endif
@@ -347,56 +347,54 @@ __device__ __forceinline__ Ptrs image_ptrs(char* ws, const Layout& L, int img) {
 // ---------------------------------------------------------------------------
 // Class bucketing of each image's candidates, on kPrepB workgroups per image (one per
 // image took 0.19 ms per batch at C2 and 0.36 ms at C4, 8 workgroups on the whole chip):
-// nms_count histograms slice b of the candidate list per class; nms_bucket places the
-// slice's rows at class offset + the earlier slices' counts (an LDS atomic within the
-// slice: the order inside a class bucket is free, every consumer sorts by (score, row));
-// nms_prep then finishes the small classes and lists the big ones, classes c = b mod kPrepB
-// on workgroup b.
+// nms_mark flags the candidate rows and histograms the row slices per class (workgroup b
+// takes slice b of the candidate list); nms_bucket places row slice b's rows at class offset
+// + the earlier slices' counts in row order (below); nms_prep then finishes the small classes
+// and lists the big ones, classes c = b mod kPrepB on workgroup b.
 __device__ __forceinline__ void prep_slice(int cnt, int b, int& i0, int& i1) {
   i0 = (int)((long long)cnt * b / kPrepB);
   i1 = (int)((long long)cnt * (b + 1) / kPrepB);
 }
 
 // nms_mark sets the flag byte of every listed candidate's row (the list is in append order; plain
-// byte stores: 32 candidates per u32 word made atomicOr on a bitmap 42 us at C2); nms_count /
-// nms_bucket then walk rows in ascending order, slice b = rows [r0, r1), so every class bucket
-// lists its rows in ascending order (a stable counting sort by class). The score sorts downstream are stable LSD passes over the score
-// digits only: equal scores keep that row order, which is the reference's (score desc, row asc).
-__global__ void __launch_bounds__(kThreads) nms_mark(ycx_nms_desc d, const int* __restrict__ cand_rows,
-                                                     const int* __restrict__ cand_counts, char* ws) {
-  const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
-  const int rows = d.rows_total;
-  const Layout L = layout(d.n, rows);
-  unsigned char* flag = reinterpret_cast<unsigned char*>(ws + L.bits) + (size_t)img * rows;
-  const int* cr = cand_rows + (size_t)img * rows;
-  int i0, i1;
-  prep_slice(min(cand_counts[img], rows), b, i0, i1);
-  for (int i = i0 + tid; i < i1; i += kThreads) flag[cr[i]] = 1;
-}
-
+// byte stores: 32 candidates per u32 word made atomicOr on a bitmap 42 us at C2) and adds the
+// class histogram of each row slice b = rows [r0, r1) (LDS counts of its list slice, then one
+// global atomic per nonzero (slice, class)); nms_bucket then walks its row slice in ascending
+// order, so every class bucket lists its rows in ascending order (a stable counting sort by
+// class). The score sorts downstream are stable LSD passes over the score digits only: equal
+// scores keep that row order, which is the reference's (score desc, row asc).
 __device__ __forceinline__ void row_slice(int rows, int b, int& r0, int& r1) {
   r0 = (int)((long long)rows * b / kPrepB);
   r1 = (int)((long long)rows * (b + 1) / kPrepB);
 }
+__device__ __forceinline__ int slice_of_row(int rows, int r) { return (int)((kPrepB * ((long long)r + 1) - 1) / rows); }
 
-__global__ void __launch_bounds__(kThreads) nms_count(ycx_nms_desc d, const ycx_cand* __restrict__ cand,
-                                                      const int* __restrict__ cand_rows,
-                                                      const int* __restrict__ cand_counts, char* ws) {
-  __shared__ int s_cnt[kMaxNc];
+__global__ void __launch_bounds__(kThreads) nms_mark(ycx_nms_desc d, const ycx_cand* __restrict__ cand,
+                                                     const int* __restrict__ cand_rows,
+                                                     const int* __restrict__ cand_counts, char* ws) {
+  __shared__ unsigned s_cnt[kPrepB * kMaxNc];  // [row slice][class]
   const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
   const int nc = d.nc, rows = d.rows_total;
   const Layout L = layout(d.n, rows);
+  unsigned char* flag = reinterpret_cast<unsigned char*>(ws + L.bits) + (size_t)img * rows;
   const ycx_cand* ci = cand + (size_t)img * rows;
-  const unsigned char* flag = reinterpret_cast<const unsigned char*>(ws + L.bits) + (size_t)img * rows;
-  int r0, r1;
-  row_slice(rows, b, r0, r1);
-  for (int c = tid; c < nc; c += kThreads) s_cnt[c] = 0;
+  const int* cr = cand_rows + (size_t)img * rows;
+  for (int k = tid; k < kPrepB * nc; k += kThreads) s_cnt[k] = 0;
+  if (b == 0 && img == 0 && tid < 64) reinterpret_cast<int*>(ws + L.hdr)[tid] = 0;  // the task-queue header (256 B)
   __syncthreads();
-  for (int r = r0 + tid; r < r1; r += kThreads)
-    if (flag[r]) atomicAdd(&s_cnt[ci[r].cls], 1);
+  int i0, i1;
+  prep_slice(min(cand_counts[img], rows), b, i0, i1);
+  for (int i = i0 + tid; i < i1; i += kThreads) {
+    const int r = cr[i];
+    flag[r] = 1;
+    atomicAdd(&s_cnt[slice_of_row(rows, r) * nc + ci[r].cls], 1u);
+  }
   __syncthreads();
-  int* bc = reinterpret_cast<int*>(ws + L.bcnt) + ((size_t)img * kPrepB + b) * kMaxNc;
-  for (int c = tid; c < nc; c += kThreads) bc[c] = s_cnt[c];
+  int* bc = reinterpret_cast<int*>(ws + L.bcnt) + (size_t)img * kPrepB * kMaxNc;  // zeroed by ycx_sort_nms
+  for (int k = tid; k < kPrepB * nc; k += kThreads) {
+    const unsigned v = s_cnt[k];
+    if (v) atomicAdd(&bc[(k / nc) * kMaxNc + k % nc], (int)v);
+  }
 }
 
 __global__ void __launch_bounds__(kThreads) nms_bucket(ycx_nms_desc d, const ycx_cand* __restrict__ cand,
@@ -434,11 +432,11 @@ __global__ void __launch_bounds__(kThreads) nms_bucket(ycx_nms_desc d, const ycx
   // rows of the slice in chunks of kThreads, thread t <-> row r0 + t: a class's rows go to its
   // bucket in row order (rank among the chunk's earlier rows of the class: earlier waves' counts
   // plus the lanes below in this wave; s_base carries the earlier chunks)
-  int rb, r_end;
-  row_slice(rows, b, rb, r_end);
   int nbits = 0;
   while ((1 << nbits) <= nc) ++nbits;  // class + 1 in [0, nc]: 0 = no candidate
   const unsigned long long lt = (1ull << lane) - 1ull;
+  int rb, r_end;
+  row_slice(rows, b, rb, r_end);
   for (int r0 = rb; r0 < r_end; r0 += kThreads) {  // uniform trip count
     const int r = r0 + tid;
     const bool valid = r < r_end && flag[r];
@@ -467,6 +465,7 @@ __global__ void __launch_bounds__(kThreads) nms_bucket(ycx_nms_desc d, const ycx
     }
     __syncthreads();
   }
+
 }
 
 __global__ void __launch_bounds__(kThreads) nms_prep(ycx_nms_desc d, const ycx_cand* __restrict__ cand, char* ws,
@@ -2085,7 +2084,6 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   if (workspace_bytes < ycx_nms_workspace_size(d)) return YCX_ERR_CAPACITY;
   YCX_CHECK_SUPPORTED(d->nc <= kMaxNc && d->rows_total <= kMaxRows);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(workspace, 0, 256, st) != hipSuccess) return YCX_ERR_LAUNCH;  // task-queue header
   char* ws = reinterpret_cast<char*>(workspace);
   const Thr t = make_thr(d->iou_thres);
   // Spatial pruning needs IoU > thr to imply overlap and bounded size ratios,
@@ -2093,10 +2091,12 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   const int all_pairs = !(d->iou_thres >= 0.0);
   const float t_lo = all_pairs ? 0.0f : (float)(fmin(d->iou_thres, 1.0) * (1.0 - 1e-3));
   const float inv_t = t_lo > 0.0f ? 1.0f / t_lo : INFINITY;
-  if (hipMemsetAsync(ws + layout(d->n, d->rows_total).bits, 0, (size_t)d->n * d->rows_total, st) != hipSuccess)
-    return YCX_ERR_LAUNCH;  // the candidate flags
-  hipLaunchKernelGGL(nms_mark, dim3(kPrepB, d->n), dim3(kThreads), 0, st, *d, cand_rows, cand_counts, ws);
-  hipLaunchKernelGGL(nms_count, dim3(kPrepB, d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws);
+  {  // the row-slice class counts and the candidate flags (adjacent in the layout)
+    const Layout L = layout(d->n, d->rows_total);
+    if (hipMemsetAsync(ws + L.bcnt, 0, L.bits + (size_t)d->n * d->rows_total - L.bcnt, st) != hipSuccess)
+      return YCX_ERR_LAUNCH;
+  }
+  hipLaunchKernelGGL(nms_mark, dim3(kPrepB, d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws);
   hipLaunchKernelGGL(nms_bucket, dim3(kPrepB, d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws);
   hipLaunchKernelGGL(nms_prep, dim3(kPrepClsB, d->n), dim3(kThreads), 0, st, *d, cand, ws, t);
   // one width for every fast class: the radix sort and the per-element loops skip the
