@@ -208,7 +208,8 @@ def roofline(det, steps, precision, replays=10):
                 forward_gap_ms=sum(o['gap_ms'] for o in ops),
                 all_conv_tflops=all_conv_tf, all_conv_ms=all_conv_ms, forward_kernel_ms=fwd_ms,
                 per_kernel={k: dict(ms=round(v['ms'], 4), launches=v['launches'],
-                                    tflops=(round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1) if v['flops'] else None))
+                                    tflops=(round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1)
+                                            if v['flops'] and v['ms'] > 0 else None))
                             for k, v in sorted(per.items(), key=lambda kv: -kv[1]['ms'])})
 
 
