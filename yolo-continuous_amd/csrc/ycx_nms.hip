@@ -61,6 +61,10 @@ constexpr int kMaxRows = 131072;  // rows (candidates) per image
 #define YCX_NMS_BIG_BLOCKS 256
 #endif
 constexpr int kBigBlocks = YCX_NMS_BIG_BLOCKS;   // nms_fast / nms_wide grid (task-strided)
+#ifndef YCX_NMS_SEARCH_BLOCKS
+#define YCX_NMS_SEARCH_BLOCKS YCX_NMS_BIG_BLOCKS
+#endif
+constexpr int kSearchBlocks = YCX_NMS_SEARCH_BLOCKS;  // nms_search grid (equal position ranges)
 constexpr int kSlots = 16;        // int suppressor ranks cached per box (64 bytes; 32 when u16)
 
 #ifdef YCX_NMS_PROFILE
@@ -2105,7 +2109,7 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   // the 24 wide and 24 fast classes of a batch then run side by side instead of in turn
   // (YCX_NMS_NO_FAST: every class on the wide path, the fast list empty)
   hipLaunchKernelGGL(nms_fast<8>, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, cand, ws, t, t_lo, inv_t, all_pairs, 1);
-  hipLaunchKernelGGL(nms_search, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
+  hipLaunchKernelGGL(nms_search, dim3(kSearchBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
   hipLaunchKernelGGL(nms_resolve, dim3(kBigBlocks), dim3(kBigThreads), 0, st, *d, ws, t, t_lo, inv_t, all_pairs);
   hipLaunchKernelGGL(nms_finish, dim3(d->n), dim3(kThreads), 0, st, *d, cand, ws, dets, keep_rows, keep_counts);
   return ycx_launch_status();
