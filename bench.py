@@ -101,7 +101,7 @@ def parse(argv=None):
                          "in pinned memory -> H2D -> ycx_letterbox_batch -> the same path; 0: skip")
     ap.add_argument("--fp16-steps", type=int, default=None,
                     help="the north_star-conforming fp16 plan (1e-3 on box / confidence tensors) timed in the same "
-                         "run after the headline leg, same steps and mode (default: --steps when --precision is "
+                         "run after the headline leg, same mode (default: min(--steps, 30) when --precision is "
                          "bf16; 0: skip); reported as value_fp16 / ms_per_step_fp16 / roofline_fp16")
     ap.add_argument("--round", default=None,
                     help="profiles/<round>/traffic.json for roofline.traffic (default: the newest round that has one)")
@@ -725,7 +725,9 @@ def main(argv=None):
     rl = roofline(det1, args.roofline_steps, args.precision) if rank == 0 else None
     flops_per_image = det1.engine.flops_per_image
     detections_last_step = int(kc.sum().item())
-    n16 = args.fp16_steps if args.fp16_steps is not None else (args.steps if args.precision == "bf16" else 0)
+    # the fp16 (north_star 1e-3) leg: at most 30 timed steps by default, so a long headline run
+    # does not double the bench's wall time
+    n16 = args.fp16_steps if args.fp16_steps is not None else (min(args.steps, 30) if args.precision == "bf16" else 0)
     fp16 = None
     if n16 > 0 and args.precision != "fp16" and not args.diag_forward_only:
         det.close()  # the headline plan's HBM back before the second plan is built

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define YCX_ABI_VERSION 8
+#define YCX_ABI_VERSION 9
 
 typedef int32_t ycx_status;
 enum {
@@ -95,6 +95,11 @@ typedef struct ycx_conv_desc {
                              * (h, w) input (nets/common.py:25-31), pooled in the conv's operand
                              * staging (1x1/s1/p0: 16-bit with cin % 64 == 0, or YCX_DT_FP8
                              * with cin % 128 == 0, r04); 0: x is the input */
+  int32_t k_split;          /* > 1: the K loop (kh*kw*cin) is cut into k_split contiguous ranges run by
+                             * separate workgroups, whose fp32 partial sums go to a caller-owned
+                             * workspace (ycx_conv2d_ws, ycx_conv_workspace_size) and are summed in a
+                             * fixed order by a second launch (bias, act, residual, store): deterministic.
+                             * 16-bit LDS-DMA tiles only (16, 18, 56), r06. 0 or 1: no split */
 } ycx_conv_desc;
 
 /* Max-pool, NHWC, pad value -inf (torch.nn.MaxPool2d semantics, floor mode).
@@ -229,6 +234,7 @@ typedef struct ycx_op {
   int32_t* cand_counts;     /* HEAD: [n], zeroed before the first level's op        */
   int32_t* status;          /* HEAD (nullable): the range guard flag, below         */
   void* out2;               /* CONV_PAIR: the second conv's output (out: the first's, nullable) */
+  void* workspace;          /* CONV with d.conv.k_split > 1: fp32 partials, >= ycx_conv_workspace_size */
 } ycx_op;
 
 int ycx_abi_version(void);
@@ -251,6 +257,14 @@ int32_t ycx_conv_tile_of(int32_t bid, int32_t nwg, int32_t n_ct, int32_t gc);
 
 ycx_status ycx_conv2d(const ycx_conv_desc* d, const void* x, const void* w,
                       const float* bias, void* y, const void* residual, void* stream);
+/* ycx_conv2d with a caller-owned workspace for d->k_split > 1 (split-K: fp32 partials of
+ * every K range, then one reduce launch; ycx_conv2d itself returns YCX_ERR_CAPACITY for
+ * k_split > 1). ycx_conv_workspace_size: the bytes it needs (0 without a split). */
+size_t ycx_conv_workspace_size(const ycx_conv_desc* d);
+ycx_status ycx_conv2d_ws(const ycx_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                         const void* residual, void* workspace, size_t workspace_bytes, void* stream);
+/* The K split the library recommends for this conv on the tile it picks (1: none). */
+int32_t ycx_conv_pick_ksplit(const ycx_conv_desc* d);
 /* Detect head 1x1 conv of one level (bf16, act none, cout = na * no <= 256,
  * out_layout YCX_OUT_NCHW_F32) fused with that level's decode + filter: appends
  * the passing rows to cand / cand_rows / cand_counts exactly as
@@ -324,7 +338,9 @@ ycx_status ycx_check_sigmoid_monotone(unsigned long long* violations, void* stre
 size_t ycx_nms_workspace_size(const ycx_nms_desc* d);
 /* Sorts each image's candidates by (class asc, score desc, row asc) — the order
  * of detect.py:124-137 with a stable torchvision sort — and runs greedy NMS per
- * class. Outputs: dets [n][max_det][7] = x1,y1,x2,y2,obj,cls_conf,cls (fp32),
+ * class. cand_rows must list each row at most once per image (both filters and the
+ * fused head decode append every passing row exactly once): the class buckets are
+ * counted per list entry and filled per distinct row. Outputs: dets [n][max_det][7] = x1,y1,x2,y2,obj,cls_conf,cls (fp32),
  * keep_rows [n][max_det] (row index, -1 padded), keep_counts [n] (not capped
  * by max_det; rows beyond max_det are dropped from dets/keep_rows). */
 ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, const int32_t* cand_rows,

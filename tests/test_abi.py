@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_metadata_without_gpu():
     from ycx import _lib
-    assert _lib.lib.ycx_abi_version() == _lib.ABI_VERSION == 8
+    assert _lib.lib.ycx_abi_version() == _lib.ABI_VERSION == 9
     for i, st in enumerate(_lib._STRUCTS):
         assert _lib.lib.ycx_struct_size(i) == ctypes.sizeof(st)
     assert _lib.lib.ycx_struct_size(99) == 0
@@ -42,7 +42,8 @@ def test_abi_metadata_without_gpu():
     assert _lib.lib.ycx_conv_tile_name(16) == b"glds_co128_px128_k64_s2"
     assert _lib.lib.ycx_conv_tile_name(50) == b"halo3x3s2_wsr_co128"
     assert _lib.lib.ycx_conv_tile_name(55) == b"wres1x1_pair"
-    assert _lib.lib.ycx_conv_tile_name(56) == b"invalid"
+    assert _lib.lib.ycx_conv_tile_name(56) == b"glds_co64_px128_k64_s3"
+    assert _lib.lib.ycx_conv_tile_name(57) == b"invalid"
     # argument validation happens before any device call
     assert _lib.lib.ycx_conv2d(None, None, None, None, None, None, None) == _lib.YCX_ERR_BAD_ARG
     assert _lib.lib.ycx_sort_nms(None, None, None, None, None, 0, None, None, None, None) == _lib.YCX_ERR_BAD_ARG

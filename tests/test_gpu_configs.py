@@ -54,7 +54,7 @@ def test_c4_1280_forward_vs_oracle(c4):
 
 def test_c4_1280_decode_nms_vs_oracle(c4):
     assert all(int(c) > 0 for c in c4['kc'])  # every image of the batch produced detections
-    for b in (0,):
+    for b in (0, 7):  # the first and the last image of the batch (verdict r05 item 8)
         rep = fused_keep_report(c4['cand'], c4['cand_rows'], c4['counts'], c4['keep'], c4['kc'], b,
                                 [h[b] for h in c4['heads']], 80, 0.3, 0.3, 1280, 50000)
         print(f"\nc4 image {b}: {rep}")

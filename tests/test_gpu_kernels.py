@@ -22,7 +22,7 @@ def _ref_conv(x_nchw, w, b, s, p, act, slope=0.1):
 
 
 def _run_conv(device, n, h, w, cin, cout, k, s, act, tile, dtype, in_extra=0, out_extra=0, residual=False,
-              layout=L.OUT_NHWC, seed=0):
+              layout=L.OUT_NHWC, seed=0, k_split=0):
     g = torch.Generator().manual_seed(seed)
     tdt = {L.DT_BF16: torch.bfloat16, L.DT_F16: torch.float16}.get(dtype, torch.float32)
     p = k // 2
@@ -50,10 +50,19 @@ def _run_conv(device, n, h, w, cin, cout, k, s, act, tile, dtype, in_extra=0, ou
     d.dtype, d.out_layout = dtype, layout
     d.res_c_off, d.res_c_stride = 0, cout
     d.tile = tile
+    d.k_split = k_split
     xd, wd, bd, yd = x.to(device), wp.contiguous().to(device), bp.to(device), y.to(device)
     rd = r.to(device) if r is not None else None
-    st = L.check(L.lib.ycx_conv2d(ctypes.byref(d), xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), yd.data_ptr(),
-                                  rd.data_ptr() if rd is not None else None, L.stream_handle(device)))
+    if k_split > 1:
+        nws = int(L.lib.ycx_conv_workspace_size(ctypes.byref(d)))
+        assert nws == k_split * n * ho * wo * cpad * 4
+        ws = torch.full((nws // 4,), float('nan'), device=device)  # every partial must be overwritten
+        L.check(L.lib.ycx_conv2d_ws(ctypes.byref(d), xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), yd.data_ptr(),
+                                    rd.data_ptr() if rd is not None else None, ws.data_ptr(), nws,
+                                    L.stream_handle(device)))
+    else:
+        L.check(L.lib.ycx_conv2d(ctypes.byref(d), xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), yd.data_ptr(),
+                                 rd.data_ptr() if rd is not None else None, L.stream_handle(device)))
     torch.cuda.synchronize()
     ref = _ref_conv(x[..., in_extra:].permute(0, 3, 1, 2).float(), wt.float(), b, s, p, act)
     if residual:
@@ -72,7 +81,7 @@ def _run_conv(device, n, h, w, cin, cout, k, s, act, tile, dtype, in_extra=0, ou
 
 TILES_BF16 = [(1, 128, 64), (2, 64, 64), (3, 64, 64), (4, 128, 64), (5, 32, 32), (6, 64, 32), (7, 128, 32),
               (9, 128, 64), (10, 64, 64), (11, 256, 128), (12, 128, 64), (13, 64, 32), (14, 128, 32), (14, 256, 32),
-              (15, 64, 64), (16, 128, 64), (17, 64, 32), (18, 64, 128)]
+              (15, 64, 64), (16, 128, 64), (17, 64, 32), (18, 64, 128), (56, 64, 128), (56, 192, 64)]
 
 
 @pytest.mark.parametrize('tile,cout,cin', TILES_BF16)
@@ -105,6 +114,54 @@ def test_conv_fp16_special_kernels(device, tile, args):
     got, ref = _run_conv(device, n, h, w, cin, cout, k, s, L.ACT_SILU if cout != 255 else L.ACT_NONE, tile,
                          L.DT_F16, in_extra=8, out_extra=extra, layout=layout)
     torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize('tile,cout', [(16, 128), (18, 64), (56, 64), (56, 192)])
+@pytest.mark.parametrize('k_split', [2, 3, 4])
+@pytest.mark.parametrize('cin,k,s', [(256, 3, 1), (512, 1, 1), (128, 3, 2), (256, 3, 2)])
+def test_conv_splitk(device, tile, cout, k_split, cin, k, s):
+    """Split-K (ycx_conv_desc.k_split, r06): K ranges on separate workgroups, fp32 partials in the
+    workspace, one ordered reduce launch with bias + act; ragged pixel tail (13 x 11), input and
+    output channel slices, the chunk-major stride-2 K order at cin 128 (tile 16)."""
+    got, ref = _run_conv(device, 2, 13, 11, cin, cout, k, s, L.ACT_SILU, tile, L.DT_BF16, in_extra=8, out_extra=16,
+                         k_split=k_split)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize('dtype,layout,residual,act', [(L.DT_BF16, L.OUT_NHWC, True, L.ACT_LEAKY),
+                                                       (L.DT_BF16, L.OUT_NHWC_UP2, False, L.ACT_NONE),
+                                                       (L.DT_F16, L.OUT_NHWC, True, L.ACT_SILU),
+                                                       (L.DT_F16, L.OUT_NHWC_UP2, False, L.ACT_SILU)])
+@pytest.mark.parametrize('tile', [16, 18])
+def test_conv_splitk_residual_up2(device, dtype, layout, residual, act, tile):
+    """The split-K reduce's store is the unsplit epilogue's (store8): residual added after the
+    activation, x2 nearest upsample, fp16 elements."""
+    cout = 128 if tile == 16 else 64
+    got, ref = _run_conv(device, 3, 20, 20, 512, cout, 3, 1, act, tile, dtype, in_extra=0, out_extra=8 if
+                         layout == L.OUT_NHWC else 0, residual=residual, layout=layout, k_split=2)
+    tol = 1e-2 if dtype == L.DT_BF16 else 2e-3
+    torch.testing.assert_close(got, ref, rtol=tol, atol=tol)
+
+
+def test_conv_splitk_rejects(device):
+    """k_split > 1 needs a workspace (YCX_ERR_CAPACITY without one) and one of the LDS-DMA
+    tiles 16 / 18 / 56 (the weight-resident, halo and fp32 tiles refuse it)."""
+    with pytest.raises(L.YcxError, match='capacity'):
+        d = L.ConvDesc()
+        d.n, d.h, d.w, d.cin, d.in_c_stride, d.ho, d.wo, d.cout, d.cout_pad, d.out_c_stride = \
+            1, 8, 8, 64, 64, 8, 8, 128, 128, 128
+        d.kh = d.kw = 1
+        d.stride, d.dtype, d.tile, d.k_split = 1, L.DT_BF16, 16, 2
+        x = torch.zeros(1, 8, 8, 64, dtype=torch.bfloat16, device=device)
+        wt = torch.zeros(128, 64, dtype=torch.bfloat16, device=device)
+        b = torch.zeros(128, device=device)
+        y = torch.zeros(1, 8, 8, 128, dtype=torch.bfloat16, device=device)
+        L.check(L.lib.ycx_conv2d(ctypes.byref(d), x.data_ptr(), wt.data_ptr(), b.data_ptr(), y.data_ptr(), None,
+                                 L.stream_handle(device)))
+    for tile in (22, 20, 8):
+        with pytest.raises(L.YcxError, match='unsupported'):
+            _run_conv(device, 2, 16, 16, 64, 128, 3 if tile == 20 else 1, 1, L.ACT_SILU, tile,
+                      L.DT_F32 if tile == 8 else L.DT_BF16, k_split=2)
 
 
 @pytest.mark.parametrize('tile', [27, 31, 33, 40, 41, 42, 43, 44, 47])

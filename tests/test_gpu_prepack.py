@@ -60,3 +60,35 @@ def test_prepack_yolov7_pair_batch_independent(device, tmp_path, precision):
     out = dst(x)
     for a, b in zip(out, ref):
         assert torch.equal(a, b)
+
+
+def test_prepack_fp16_overflow_raises(device, tmp_path):
+    """an fp16 plan bound to prepacked weights cannot re-plan itself in bf16 (that
+    would fold the module's own parameters, not the file's), so a non-finite forward raises
+    YcxRangeError instead of returning inf / NaN heads; an in-range prepacked fp16 forward
+    returns the packing model's heads bit for bit."""
+    from ycx import _lib as L
+    src, sd = make_model('yolov7-tiny', 1, 0, 'fp16')
+    src.to(device)
+    x = synthetic_images(2, 3, 160, 160, seed=9).to(device)
+    ref = [o.clone() for o in src(x)]
+    ok_path = str(tmp_path / "tiny_fp16.safetensors")
+    src.save_prepacked(ok_path, (160, 160))
+    dst, _ = make_model('yolov7-tiny', 1, 0, 'bf16')
+    dst.load_prepacked(ok_path)
+    dst.to(device)
+    for a, b in zip(dst(x), ref):
+        assert torch.equal(a, b)
+    bn = [k for k in sd if k.endswith('.bn.weight')][2]
+    big = dict(sd)
+    big[bn] = sd[bn] * 1e5  # that layer's activations pass 65504: inf in fp16
+    src.load_state_dict(big)
+    src.to(device)
+    bad_path = str(tmp_path / "tiny_fp16_big.safetensors")
+    src.save_prepacked(bad_path, (160, 160))
+    bad, _ = make_model('yolov7-tiny', 1, 0, 'bf16')
+    bad.load_prepacked(bad_path)
+    bad.to(device)
+    assert bad.precision == 'fp16'
+    with pytest.raises(L.YcxRangeError, match='prepacked'):
+        bad(x)

@@ -13,7 +13,7 @@ case "$job" in
     timeout -k 10 900 $PYT -s "$@" > "$O/tests.log" 2>&1; rc=$?
     tail -30 "$O/tests.log"; exit $rc ;;
   bench)  # the default bench + the per-op gap table
-    YCX_BENCH_KERNELS=$O/ops.json timeout -k 10 400 python bench.py "$@" > "$O/bench.log" 2>&1 || { tail -20 "$O/bench.log"; exit 1; }
+    YCX_BENCH_KERNELS=$O/ops.json timeout -k 10 600 python bench.py "$@" > "$O/bench.log" 2>&1 || { tail -20 "$O/bench.log"; exit 1; }
     tail -1 "$O/bench.log" | cut -c1-3000
     python tools/op_gap.py "$O/ops.json" 25 > "$O/op_gap.md" && head -40 "$O/op_gap.md" ;;
   full)  # the round-end sequence: GPU suite, smoke, bench
@@ -21,7 +21,7 @@ case "$job" in
     tail -2 "$O/gputests.log"
     timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { tail -20 "$O/smoke.log"; exit 1; }
     tail -1 "$O/smoke.log"
-    YCX_BENCH_KERNELS=$O/ops.json timeout -k 10 400 python bench.py > "$O/bench.log" 2>&1 || { tail -20 "$O/bench.log"; exit 1; }
+    YCX_BENCH_KERNELS=$O/ops.json timeout -k 10 600 python bench.py > "$O/bench.log" 2>&1 || { tail -20 "$O/bench.log"; exit 1; }
     tail -1 "$O/bench.log" | cut -c1-1500
     python tools/op_gap.py "$O/ops.json" > "$O/op_gap.md" ;;
   probe)  # a probe script: bash tools/job.sh probe tests/probes/x.py args

@@ -66,6 +66,8 @@ struct ConvArgs {
   int pool;                    // x is the (2H, 2W) map of a fused k2 s2 max-pool (ycx_conv_desc.in_pool)
   int gc;                      // LDS-DMA tiles: channel groups of the XCD region map (ycx_tile_of)
   long long out_bytes;         // extent of y the descriptor implies (YCX_DEBUG_BOUNDS store checks)
+  int ks;                      // split-K ranges (ycx_conv_desc.k_split; 1: none)
+  float* part;                 // ks > 1: fp32 partials [ks][M][Cout_pad] (the caller's workspace)
 };
 // a store of nb bytes at ptr inside the output extent of args A (always true in release builds)
 #define YCX_OUT_OK(A, ptr, nb) \
@@ -703,8 +705,12 @@ __device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const fl
 // weight DMA of t + 1 and four 16-byte global loads per pixel row (the 2x2 window),
 // and after step t's MFMAs takes their max and writes it to the LDS slot where the
 // activation DMA would have put it. The pooled map never reaches HBM.
+// SK (split-K, ycx_conv_desc.k_split, r06): gridDim = tiles x a.ks; workgroup (slice, tile) runs
+// K steps [slice nsteps / ks, (slice + 1) nsteps / ks) of its tile and stores the raw fp32 sums
+// to a.part[slice][M][Cout_pad]; splitk_reduce adds the slices in order, then bias / act /
+// residual / store. Logical ids are slice-major, so an XCD's range is mostly one slice.
 template <int BM, int BN, int WM, int WN, bool TT, int NST, int NSB = NST, bool HEAD = false, bool POOL = false,
-          bool KCM = false>
+          bool KCM = false, bool SK = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadArgs hd) {
   constexpr int NW = WM * WN;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
@@ -736,10 +742,17 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   const unsigned long long st_start = stamp_issue();
 #endif
   const int wm = wid / WN, wn = wid % WN;
-  const int L = ycx_xcd_remap(blockIdx.x, a.nwg);
+  static_assert(!SK || (!TT && !POOL && !HEAD), "split-K: plain im2col steps");
+  int L = ycx_xcd_remap(blockIdx.x, SK ? (int)gridDim.x : a.nwg), slice = 0;
+  if constexpr (SK) {
+    slice = L / a.nwg;
+    L -= slice * a.nwg;
+  }
   int ct, pt;
   ycx_tile_of(L, a.n_ct, a.nwg / a.n_ct, a.gc, ct, pt);
   const int co0 = ct * BM, px0 = pt * BN;
+  // this workgroup's K steps [s_lo, s_lo + nt)
+  const int s_lo = SK ? slice * a.nsteps / a.ks : 0;
   const int lrow = lane >> 3, pch = lane & 7;  // row within the 8-row wave slab, physical chunk
 
   // Buffer descriptors (raw, stride 0): 32-bit byte offsets, and an offset past
@@ -781,6 +794,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   int i_ky = 0, i_kx = 0, i_cb = 0;  // K position (first tap) of the next stage to issue
   const int ntaps = a.KH * a.KW;
   int i_tap = 0;
+  if constexpr (SK) {
+    if (!KCM) {
+      const int cpt = a.Cin / BK, tap = s_lo / cpt;
+      i_cb = (s_lo - tap * cpt) * BK;
+      i_ky = tap / a.KW;
+      i_kx = tap - i_ky * a.KW;
+    }
+  }
   // Stride-2 3x3s (Cin % 64 == 0) walk K channel-chunk-major with the taps that read the same
   // input pixels next to each other: (ky, kx) = (0,0) (0,2) (0,1) (2,0) (2,2) (2,1) (1,0) (1,2) (1,1)
   // (kx 0 / 2 of neighbouring output pixels share the odd input columns, ky 0 / 2 of neighbouring
@@ -793,12 +814,13 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   constexpr bool kcm = KCM;
   static_assert(!KCM || (!TT && !POOL && !HEAD), "K order for plain 3x3/s2 steps");
   constexpr unsigned long long kTapS2 = 0x453786201ull;  // 4 bits per position: taps 0 2 1 6 8 7 3 5 4
-  auto k_of = [&](int s) {  // K element offset of step s in the packed weight row
+  auto k_of = [&](int s) {  // K element offset of step s_lo + s in the packed weight row
+    s += s_lo;
     if (!kcm) return s * BK;
     const int c = s / 9, tp = (int)((kTapS2 >> (4 * (s - 9 * c))) & 15);
     return tp * a.Cin + c * BK;
   };
-  int i_s = 0;  // kcm: B steps issued
+  int i_s = s_lo;  // kcm: B steps issued (absolute)
   auto a_slot = [&](int buf) { return SPLIT ? smem + buf * A_BYTES : smem + buf * STAGE; };
   auto b_slot = [&](int buf) { return SPLIT ? smem + NST * A_BYTES + buf * B_BYTES : smem + buf * STAGE + A_BYTES; };
   auto issueA = [&](int s, int buf) {
@@ -891,7 +913,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   } else if constexpr (FM % 2 == 0 && !POOL) {  // POOL: no registers to spare, loaded after the loop
     if (perm) bias8_prefetch<FM>(a, co0 + wm * TM, lane, bpre);
   }
-  const int nt = a.nsteps;
+  const int nt = SK ? (slice + 1) * a.nsteps / a.ks - s_lo : a.nsteps;
   if constexpr (POOL) {
     issueA(0, 0);
     loadB();
@@ -988,6 +1010,24 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
 #endif
   }
   bool done = false;
+  if constexpr (SK) {  // raw fp32 sums: 8 consecutive channels of one pixel per lane and fragment pair
+    static_assert(FM % 2 == 0, "split-K partials use the permuted rows");
+    float* P = a.part + (size_t)slice * a.M * a.Cout_pad;
+#pragma unroll
+    for (int k = 0; k < FM / 2; ++k) {
+      const int co = co0 + wm * TM + 32 * k + 8 * (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int p = px0 + wn * TN + j * 16 + (lane & 15);
+        if (p < a.M) {
+          float* q = P + (size_t)p * a.Cout_pad + co;
+          *reinterpret_cast<f32x4*>(q) = acc[2 * k][j];
+          *reinterpret_cast<f32x4*>(q + 4) = acc[2 * k + 1][j];
+        }
+      }
+    }
+    done = true;
+  }
   if constexpr (HEAD) {
     // every wave is past its last fragment read: the stages become the logit tile
     __syncthreads();
@@ -1012,14 +1052,15 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     head_decode_tile<BN>(a, hd, T, HEAD_LDT, px0);
     done = true;
   }
-  if constexpr (FM % 2 == 0 && !HEAD) {
+  if constexpr (FM % 2 == 0 && !HEAD && !SK) {
     if (perm) {
       if constexpr (POOL) bias8_prefetch<FM>(a, co0 + wm * TM, lane, bpre);
       epilogue_regs8<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane, bpre);
       done = true;
     }
   }
-  if (!HEAD && !done) epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
+  if constexpr (!HEAD && !SK)
+    if (!done) epilogue_regs<FM, FN>(a, acc, co0 + wm * TM, px0 + wn * TN, lane);
 #ifdef YCX_GLDS_STAMP
   {
     const unsigned long long e = stamp_issue();
@@ -1035,6 +1076,36 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
   }
   if (tid == 0) atomicAdd(&g_glds_stamp[128], 1ull);
 #endif
+}
+
+// Split-K combine (r06): the a.ks fp32 partial sums of every (pixel, 8 channels) added in
+// slice order, then bias + act (+ residual, x2 upsample) and the 16-byte store of the
+// unsplit epilogue (store8). One thread per (pixel, 8-channel group): consecutive threads
+// read consecutive 32-byte runs of a partial row.
+template <int ACT>
+__global__ void __launch_bounds__(256) splitk_reduce(ConvArgs a) {
+  const int ng = a.Cout >> 3;  // cout % 8 == 0
+  const long long total = (long long)a.M * ng, slab = (long long)a.M * a.Cout_pad;
+  const float nl2e = silu_nl2e();
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int p = (int)(e / ng), co = (int)(e - (long long)p * ng) * 8;
+    const float* q = a.part + (size_t)p * a.Cout_pad + co;
+    f32x4 s0 = *reinterpret_cast<const f32x4*>(q), s1 = *reinterpret_cast<const f32x4*>(q + 4);
+    for (int k = 1; k < a.ks; ++k) {
+      q += slab;
+      s0 += *reinterpret_cast<const f32x4*>(q);
+      s1 += *reinterpret_cast<const f32x4*>(q + 4);
+    }
+    const f32x4 x0 = act4_t<ACT>(s0 + *reinterpret_cast<const f32x4*>(a.bias + co), a.slope, nl2e);
+    const f32x4 x1 = act4_t<ACT>(s1 + *reinterpret_cast<const f32x4*>(a.bias + co + 4), a.slope, nl2e);
+    float v[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = x0[r];
+      v[4 + r] = x1[r];
+    }
+    store8<elt_t>(a, p, co, v);
+  }
 }
 
 // -------------------------------------------------------------------------
@@ -3188,6 +3259,8 @@ ConvArgs make_args(const ycx_conv_desc* d, const void* x, const void* w, const f
   a.nsteps = 0; a.n_ct = 0; a.nwg = 0; a.gc = 0;
   a.out_scale = d->out_scale; a.res_scale = d->res_scale;
   a.pool = d->in_pool;
+  a.ks = d->k_split > 1 ? d->k_split : 1;
+  a.part = nullptr;
   {
     const long long es = d->dtype == YCX_DT_F32 ? 4 : d->dtype == YCX_DT_FP8 ? 1 : 2;
     const long long px = (long long)d->n * d->ho * d->wo * (d->out_layout == YCX_OUT_NHWC_UP2 ? 4 : 1);
@@ -3258,6 +3331,7 @@ const TileInfo kTiles[] = {
     {256, 128, 64, "retired_glds16w_co256_px128_s3"},
     {128, 256, 64, "retired_glds16w_co128_px256_s3"},
     {256, 64, 64, "wres1x1_pair"},  // 55: ycx_conv2d_pair only (two chained 1x1 convs)
+    {64, 128, 64, "glds_co64_px128_k64_s3"},  // 56: tile 18 with a three-stage ring (r06)
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -3349,6 +3423,29 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
     }
   }
   if (a.pool) return YCX_ERR_UNSUPPORTED;
+  if constexpr (!TT && NSB == NST && BN == 128 && (BM == 128 || BM == 64)) {  // tiles 16, 18, 56: split-K
+    if (a.ks > 1) {
+      if (!a.part || a.out_layout == YCX_OUT_NCHW_F32 || a.ks > a.nsteps) return YCX_ERR_UNSUPPORTED;
+      const dim3 g(a.nwg * a.ks), b(WM * WN * 64);
+      if (a.S == 2 && a.KH == 3 && a.KW == 3 && a.Cin == 128 && BM == 128 && NST == 2)
+        hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, false, NST, NST, false, false, true, true>), g, b, 0, st, a,
+                           HeadArgs{});
+      else
+        hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, false, NST, NST, false, false, false, true>), g, b, 0, st,
+                           a, HeadArgs{});
+      ycx_status s = ycx_launch_status();
+      if (s != YCX_OK) return s;
+      const long long total = (long long)a.M * (a.Cout >> 3);
+      const dim3 rg((unsigned)std::min<long long>((total + 255) / 256, 4096)), rb(256);
+      switch (a.act) {
+        case YCX_ACT_SILU: hipLaunchKernelGGL(splitk_reduce<YCX_ACT_SILU>, rg, rb, 0, st, a); break;
+        case YCX_ACT_LEAKY: hipLaunchKernelGGL(splitk_reduce<YCX_ACT_LEAKY>, rg, rb, 0, st, a); break;
+        default: hipLaunchKernelGGL(splitk_reduce<YCX_ACT_NONE>, rg, rb, 0, st, a); break;
+      }
+      return ycx_launch_status();
+    }
+  }
+  if (a.ks > 1) return YCX_ERR_UNSUPPORTED;
   if constexpr (!TT && NST == 2 && NSB == 2 && BM == 128 && BN == 128) {  // tile 16 on a 3x3/s2 at Cin 128
     if (a.S == 2 && a.KH == 3 && a.KW == 3 && a.Cin == 128) {  // Cin 256 / 512: slower
       hipLaunchKernelGGL((conv_bf16_glds<BM, BN, WM, WN, false, 2, 2, false, false, true>), dim3(a.nwg),
@@ -3652,8 +3749,8 @@ extern "C" int32_t ycx_conv_pick_tile(const ycx_conv_desc* d) {
 }
 
 // the fp16 build's entry points (ycx_conv.hip compiled with -DYCX_ELT_F16)
-extern "C" ycx_status ycx_conv2d_f16(const ycx_conv_desc*, const void*, const void*, const float*, void*,
-                                     const void*, void*);
+extern "C" ycx_status ycx_conv2d_ws_f16(const ycx_conv_desc*, const void*, const void*, const float*, void*,
+                                        const void*, void*, size_t, void*);
 extern "C" ycx_status ycx_conv2d_head_f16(const ycx_conv_desc*, const ycx_head_desc*, const void*, const void*,
                                           const float*, float*, ycx_cand*, int32_t*, int32_t*, int32_t*, void*);
 extern "C" ycx_status ycx_stem_conv_f16(const ycx_conv_desc*, const float*, const float*, const float*, void*,
@@ -3672,10 +3769,48 @@ extern "C" ycx_status ycx_stem_conv2_f16(const ycx_conv_desc*, const ycx_conv_de
   } while (0)
 #endif
 
+#ifndef YCX_ELT_F16
+extern "C" size_t ycx_conv_workspace_size(const ycx_conv_desc* d) {
+  if (!d || d->k_split <= 1 || d->n <= 0 || d->ho <= 0 || d->wo <= 0 || d->cout_pad <= 0) return 0;
+  return (size_t)d->k_split * d->n * d->ho * d->wo * d->cout_pad * sizeof(float);
+}
+
+// Split-K pick (r06): none by default; -DYCX_KSPLIT_AUTO builds the
+// heuristic under test (LDS-DMA tiles 16 / 18 with fewer than YCX_KSPLIT_AUTO workgroups
+// and >= 16 K steps: split so the grid reaches that many).
+extern "C" int32_t ycx_conv_pick_ksplit(const ycx_conv_desc* d) {
+  if (!d || (d->dtype != YCX_DT_BF16 && d->dtype != YCX_DT_F16) || d->in_pool || d->out_layout == YCX_OUT_NCHW_F32)
+    return 1;
+#ifdef YCX_KSPLIT_AUTO
+  const int tile = d->tile ? d->tile : pick_tile(d, d->res_c_stride == 0);
+  if (tile != 16 && tile != 18 && tile != 56) return 1;
+  const int bm = kTiles[tile].bm;
+  const long long nwg = (long long)(d->cout_pad / bm) * ((long long)d->n * d->ho * d->wo + 127) / 128;
+  const int nsteps = d->kh * d->kw * (d->cin / 64);
+  int ks = 1;
+  while (nwg * (ks + 1) <= YCX_KSPLIT_AUTO && nsteps / (ks + 1) >= 8 && ks < 4) ++ks;
+  if (nwg * ks < YCX_KSPLIT_AUTO / 2 && nsteps >= 32) ks = std::max(ks, 2);
+  return nsteps >= 16 ? ks : 1;
+#else
+  return 1;
+#endif
+}
+#endif
+
+extern "C" ycx_status YCX_SFX(ycx_conv2d_ws)(const ycx_conv_desc*, const void*, const void*, const float*, void*,
+                                             const void*, void*, size_t, void*);
 extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x, const void* w, const float* bias,
                                           void* y, const void* residual, void* stream) {
-  YCX_TO_F16(d && d->dtype == YCX_DT_F16, ycx_conv2d_f16(d, x, w, bias, y, residual, stream));
+  return YCX_SFX(ycx_conv2d_ws)(d, x, w, bias, y, residual, nullptr, 0, stream);
+}
+
+extern "C" ycx_status YCX_SFX(ycx_conv2d_ws)(const ycx_conv_desc* d, const void* x, const void* w, const float* bias,
+                                             void* y, const void* residual, void* workspace, size_t workspace_bytes,
+                                             void* stream) {
+  YCX_TO_F16(d && d->dtype == YCX_DT_F16,
+             ycx_conv2d_ws_f16(d, x, w, bias, y, residual, workspace, workspace_bytes, stream));
   YCX_CHECK_ARG(d && x && w && bias && y);
+  YCX_CHECK_ARG(d->k_split >= 0);
   YCX_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->cin > 0 && d->cout > 0 && d->ho > 0 && d->wo > 0);
   YCX_CHECK_ARG(d->kh > 0 && d->kw > 0 && d->stride > 0 && d->pad >= 0);
   YCX_CHECK_ARG(d->cout_pad >= d->cout && d->in_c_off >= 0 && d->in_c_off + d->cin <= d->in_c_stride);
@@ -3707,6 +3842,13 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x,
 
   int tile = d->tile ? d->tile : pick_tile(d, residual == nullptr);  // tile 22 stores no residual
   YCX_CHECK_SUPPORTED(tile > 0 && tile < kNumTiles);
+  if (a.ks > 1) {  // split-K: the two-stage / three-stage LDS-DMA tiles, 16-bit, NHWC outputs
+    YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_ELT && !d->in_pool && d->out_layout != YCX_OUT_NCHW_F32 &&
+                        (tile == 16 || tile == 18 || tile == 56) && d->cin % 64 == 0 && d->k_split <= 16);
+    if (!workspace || workspace_bytes < ycx_conv_workspace_size(d)) return YCX_ERR_CAPACITY;
+    YCX_CHECK_SUPPORTED((long long)d->k_split * d->n * d->ho * d->wo * d->cout_pad < (1LL << 31));
+    a.part = reinterpret_cast<float*>(workspace);
+  }
   YCX_CHECK_SUPPORTED(!d->in_pool || tile == 16 || tile == 18 || tile == 25 || tile == 34 || tile == 35);
   const TileInfo& t = kTiles[tile];
   YCX_CHECK_SUPPORTED(d->cin % t.bk == 0 && d->cout_pad % t.bm == 0);
@@ -3759,6 +3901,7 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d)(const ycx_conv_desc* d, const void* x,
     case 48: return launch_halo<64, 2, 4, 2, 8, 40>(a, st);      // band halo tiles (40-wide maps)
     case 49: return launch_halo<128, 4, 2, 2, 4, 40>(a, st);
     case 50: return launch_s2wsr(a, st);
+    case 56: return launch_glds<64, 128, 1, 8, false, 3>(a, st);
     default: return YCX_ERR_UNSUPPORTED;
   }
 }

@@ -422,7 +422,8 @@ extern "C" ycx_status ycx_quantize_fp8(const float* x, void* y, int64_t n, float
 static ycx_status run_one(const ycx_op& op, void* stream) {
   switch (op.kind) {
     case YCX_OP_CONV:
-      return ycx_conv2d(&op.d.conv, op.in, op.weight, op.bias, op.out, op.residual, stream);
+      return ycx_conv2d_ws(&op.d.conv, op.in, op.weight, op.bias, op.out, op.residual, op.workspace,
+                           op.workspace ? ycx_conv_workspace_size(&op.d.conv) : 0, stream);
     case YCX_OP_STEM:
       return ycx_stem_conv(&op.d.conv, (const float*)op.in, (const float*)op.weight, op.bias, op.out, stream);
     case YCX_OP_POOL:

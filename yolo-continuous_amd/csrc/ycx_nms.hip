@@ -132,7 +132,7 @@ __host__ __device__ inline int next_pow2(int v) {
 
 __host__ __device__ inline size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
 
-__host__ __device__ inline Layout layout(int n, int rows) {
+__host__ __device__ inline Layout layout(int n, int rows, int nc) {
   Layout L;
   L.max_tasks = rows / (kRegMax + 1) + 1;
   L.hdr = 0;
@@ -143,7 +143,8 @@ __host__ __device__ inline Layout layout(int n, int rows) {
   L.fframes = al(L.wcells + (size_t)n * L.max_wide * wide_cells_bytes());
   L.fcells = al(L.fframes + (size_t)kSplitTasks * wframe_bytes());
   L.bcnt = al(L.fcells + (size_t)kSplitTasks * fast_cells_bytes());
-  L.bits = al(L.bcnt + (size_t)n * kPrepB * kMaxNc * 4);  // per image: a candidate flag byte per row
+  L.bits = al(L.bcnt + (size_t)n * kPrepB * nc * 4);  // row-slice class counts [n][kPrepB][nc]; then per
+                                                      // image a candidate flag byte per row
   L.per_image_base = al(L.bits + (size_t)n * rows);
   size_t o = 0;
   // keys: a class at bucket offset `off` with S rows sorts at keys + 2*off; its
@@ -376,10 +377,10 @@ __device__ __forceinline__ int slice_of_row(int rows, int r) { return (int)((kPr
 __global__ void __launch_bounds__(kThreads) nms_mark(ycx_nms_desc d, const ycx_cand* __restrict__ cand,
                                                      const int* __restrict__ cand_rows,
                                                      const int* __restrict__ cand_counts, char* ws) {
-  __shared__ unsigned s_cnt[kPrepB * kMaxNc];  // [row slice][class]
+  extern __shared__ unsigned s_cnt[];  // [row slice][class]: kPrepB * nc counters (dynamic LDS)
   const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
   const int nc = d.nc, rows = d.rows_total;
-  const Layout L = layout(d.n, rows);
+  const Layout L = layout(d.n, rows, d.nc);
   unsigned char* flag = reinterpret_cast<unsigned char*>(ws + L.bits) + (size_t)img * rows;
   const ycx_cand* ci = cand + (size_t)img * rows;
   const int* cr = cand_rows + (size_t)img * rows;
@@ -394,10 +395,10 @@ __global__ void __launch_bounds__(kThreads) nms_mark(ycx_nms_desc d, const ycx_c
     atomicAdd(&s_cnt[slice_of_row(rows, r) * nc + ci[r].cls], 1u);
   }
   __syncthreads();
-  int* bc = reinterpret_cast<int*>(ws + L.bcnt) + (size_t)img * kPrepB * kMaxNc;  // zeroed by ycx_sort_nms
+  int* bc = reinterpret_cast<int*>(ws + L.bcnt) + (size_t)img * kPrepB * nc;  // zeroed by ycx_sort_nms
   for (int k = tid; k < kPrepB * nc; k += kThreads) {
     const unsigned v = s_cnt[k];
-    if (v) atomicAdd(&bc[(k / nc) * kMaxNc + k % nc], (int)v);
+    if (v) atomicAdd(&bc[k], (int)v);
   }
 }
 
@@ -409,15 +410,15 @@ __global__ void __launch_bounds__(kThreads) nms_bucket(ycx_nms_desc d, const ycx
   __shared__ unsigned short s_wc[NW][kMaxNc];  // per (wave, class) rows of the current chunk
   const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int nc = d.nc, rows = d.rows_total;
-  const Layout L = layout(d.n, rows);
+  const Layout L = layout(d.n, rows, d.nc);
   const Ptrs P = image_ptrs(ws, L, img);
   const ycx_cand* ci = cand + (size_t)img * rows;
   const unsigned char* flag = reinterpret_cast<const unsigned char*>(ws + L.bits) + (size_t)img * rows;
-  const int* bc = reinterpret_cast<const int*>(ws + L.bcnt) + (size_t)img * kPrepB * kMaxNc;
+  const int* bc = reinterpret_cast<const int*>(ws + L.bcnt) + (size_t)img * kPrepB * nc;
   for (int c = tid; c < nc; c += kThreads) {
     int tot = 0, before = 0;
     for (int q = 0; q < kPrepB; ++q) {
-      const int v = bc[(size_t)q * kMaxNc + c];
+      const int v = bc[(size_t)q * nc + c];
       before += q < b ? v : 0;
       tot += v;
     }
@@ -478,7 +479,7 @@ __global__ void __launch_bounds__(kThreads) nms_prep(ycx_nms_desc d, const ycx_c
   __shared__ int s_next;
   const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int nc = d.nc, rows = d.rows_total;
-  const Layout L = layout(d.n, rows);
+  const Layout L = layout(d.n, rows, d.nc);
   const Ptrs P = image_ptrs(ws, L, img);
   Hdr* hdr = reinterpret_cast<Hdr*>(ws + L.hdr);
   Task* tasks = reinterpret_cast<Task*>(ws + L.tasks);
@@ -592,8 +593,10 @@ constexpr int kFCellBytes = ((kFCells + 1) / 2 * 4 + 255) & ~255;  // u16 end po
 // every (digit, thread) its first output slot, the keys are scattered to dst in LDS and read
 // back blocked. Stable because a thread's elements keep their order inside a digit and
 // threads are ordered inside each digit, i.e. the (tid, i) order of the input is preserved.
-// The whole order is the 64-bit key order restricted to bits [lo, 64): with lo = 13 the fast
-// path's (score desc, row asc) order (the low 13 bits only name the element).
+// The whole order is the 64-bit key order restricted to bits [lo, 64). The fast path passes
+// lo = 32: it sorts the score bits [32, 64) only, and the (score desc, row asc) order on equal
+// scores comes from the stability of the passes over the input order, which nms_bucket makes
+// ascending by row within every class (the low bits only name the element).
 template <int E>
 __device__ void radix_sort_regs(unsigned long long (&key)[E], int S, int lo, unsigned long long* dst,
                                 unsigned short* T, int* s_w, unsigned long long* s_msk) {
@@ -1192,7 +1195,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   __shared__ unsigned long long s_msk[2];   // radix sort: AND / OR of the keys
   const int tid = threadIdx.x;
   const int rows = d.rows_total;
-  const Layout L = layout(d.n, rows);
+  const Layout L = layout(d.n, rows, d.nc);
   const Hdr* hdr = reinterpret_cast<const Hdr*>(ws + L.hdr);
   const Task* tasks = reinterpret_cast<const Task*>(ws + L.tasks);
   const int ntasks = hdr->ntasks, nwide = with_wide ? hdr->nwide : 0;
@@ -1667,7 +1670,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   __shared__ __attribute__((aligned(16))) char smem[kBigLds];
   __shared__ int s_lv[kFLevels][5];
   unsigned* cells = reinterpret_cast<unsigned*>(smem);
-  const Layout L = layout(d.n, d.rows_total);
+  const Layout L = layout(d.n, d.rows_total, d.nc);
   const BigList bl = big_list(ws, L, d.n);
   const int nt = bl.size();
   long long tot = 0;
@@ -1990,7 +1993,7 @@ __global__ void __launch_bounds__(kBigThreads) __attribute__((amdgpu_waves_per_e
   __shared__ int s_lv[kFLevels][5];
   __shared__ int s_w[kBigThreads / 64];
   __shared__ int s_flag;
-  const Layout L = layout(d.n, d.rows_total);
+  const Layout L = layout(d.n, d.rows_total, d.nc);
   const BigList bl = big_list(ws, L, d.n);
   for (int t = blockIdx.x; t < bl.size(); t += gridDim.x) {
     if (t < bl.nwide) {
@@ -2010,7 +2013,7 @@ __global__ void __launch_bounds__(kThreads) nms_finish(ycx_nms_desc d, const ycx
   __shared__ int s_total;
   const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nc = d.nc, rows = d.rows_total;
-  const Layout L = layout(d.n, rows);
+  const Layout L = layout(d.n, rows, d.nc);
   const Ptrs P = image_ptrs(ws, L, img);
   const ycx_cand* ci = cand + (size_t)img * rows;
   for (int c = tid; c < nc; c += kThreads) { s_kc[c] = P.kc[c]; s_off[c] = P.offs[c]; }
@@ -2076,7 +2079,7 @@ extern "C" int ycx_nms_prof_read(unsigned long long* out, int reset) {  // out[0
 
 extern "C" size_t ycx_nms_workspace_size(const ycx_nms_desc* d) {
   if (!d || d->n <= 0 || d->rows_total <= 0) return 0;
-  const Layout L = layout(d->n, d->rows_total);
+  const Layout L = layout(d->n, d->rows_total, d->nc);
   return L.per_image_base + L.per_image * (size_t)d->n;
 }
 
@@ -2096,11 +2099,12 @@ extern "C" ycx_status ycx_sort_nms(const ycx_nms_desc* d, const ycx_cand* cand, 
   const float t_lo = all_pairs ? 0.0f : (float)(fmin(d->iou_thres, 1.0) * (1.0 - 1e-3));
   const float inv_t = t_lo > 0.0f ? 1.0f / t_lo : INFINITY;
   {  // the row-slice class counts and the candidate flags (adjacent in the layout)
-    const Layout L = layout(d->n, d->rows_total);
+    const Layout L = layout(d->n, d->rows_total, d->nc);
     if (hipMemsetAsync(ws + L.bcnt, 0, L.bits + (size_t)d->n * d->rows_total - L.bcnt, st) != hipSuccess)
       return YCX_ERR_LAUNCH;
   }
-  hipLaunchKernelGGL(nms_mark, dim3(kPrepB, d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws);
+  hipLaunchKernelGGL(nms_mark, dim3(kPrepB, d->n), dim3(kThreads), (size_t)kPrepB * d->nc * sizeof(unsigned), st, *d,
+                     cand, cand_rows, cand_counts, ws);
   hipLaunchKernelGGL(nms_bucket, dim3(kPrepB, d->n), dim3(kThreads), 0, st, *d, cand, cand_rows, cand_counts, ws);
   hipLaunchKernelGGL(nms_prep, dim3(kPrepClsB, d->n), dim3(kThreads), 0, st, *d, cand, ws, t);
   // one width for every fast class: the radix sort and the per-element loops skip the

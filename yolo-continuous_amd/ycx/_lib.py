@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see above)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("YCX_LIB", os.path.join(_HERE, "libycx_hip.so"))
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # ---- enums (ycx.h) ----
 YCX_OK, YCX_ERR_BAD_ARG, YCX_ERR_UNSUPPORTED, YCX_ERR_LAUNCH, YCX_ERR_CAPACITY = 0, 1, 2, 3, 4
@@ -36,7 +36,7 @@ class ConvDesc(ctypes.Structure):
         "ho", "wo", "cout", "cout_pad", "out_c_off", "out_c_stride",
         "kh", "kw", "stride", "pad", "act")] + [("leaky_slope", ctypes.c_float)] + [
         (n, _i32) for n in ("dtype", "out_layout", "res_c_off", "res_c_stride", "tile")] + [
-        ("out_scale", ctypes.c_float), ("res_scale", ctypes.c_float), ("in_pool", _i32)]
+        ("out_scale", ctypes.c_float), ("res_scale", ctypes.c_float), ("in_pool", _i32), ("k_split", _i32)]
 
 
 class PoolDesc(ctypes.Structure):
@@ -97,7 +97,7 @@ class Op(ctypes.Structure):
                 ("out", ctypes.c_void_p), ("residual", ctypes.c_void_p),
                 ("weight2", ctypes.c_void_p), ("bias2", ctypes.c_void_p),
                 ("cand", ctypes.c_void_p), ("cand_rows", ctypes.c_void_p), ("cand_counts", ctypes.c_void_p),
-                ("status", ctypes.c_void_p), ("out2", ctypes.c_void_p)]
+                ("status", ctypes.c_void_p), ("out2", ctypes.c_void_p), ("workspace", ctypes.c_void_p)]
 
 
 class LetterboxDesc(ctypes.Structure):
@@ -122,6 +122,9 @@ _SIGS = [
     ("ycx_conv_pick_tile", _i32, [ctypes.POINTER(ConvDesc)]),
     ("ycx_conv_tile_of", _i32, [_i32, _i32, _i32, _i32]),
     ("ycx_conv2d", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP]),
+    ("ycx_conv_workspace_size", ctypes.c_size_t, [ctypes.POINTER(ConvDesc)]),
+    ("ycx_conv2d_ws", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_size_t, _VP]),
+    ("ycx_conv_pick_ksplit", _i32, [ctypes.POINTER(ConvDesc)]),
     ("ycx_conv2d_head", _i32, [ctypes.POINTER(ConvDesc), ctypes.POINTER(HeadDesc), _VP, _VP, _VP, _VP, _VP, _VP,
                                _VP, _VP, _VP]),
     ("ycx_stem_conv", _i32, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP]),

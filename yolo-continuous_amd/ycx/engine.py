@@ -271,6 +271,8 @@ def lower_module(g: Graph, m, x):
 # tile 16 by 24 where cout_pad allows, else 26 (never set in the product path).
 _TILE_MAP = {int(a): [int(t) for t in b.split('/')] for a, b in
              (kv.split(':') for kv in os.environ.get('YCX_TILE_MAP', '').split(',') if kv)}
+# A/B switch: YCX_NO_KSPLIT=1 runs every conv unsplit even where ycx_conv_pick_ksplit splits its K loop
+_NO_KSPLIT = bool(os.environ.get('YCX_NO_KSPLIT'))
 
 
 def cascade_fits(h, w, c, esz):
@@ -642,6 +644,7 @@ class Engine:
             b.tensor = torch.empty((b.n, b.h, b.w, b.c), dtype=dt, device=dev)
             self.buffers.append(b.tensor)
         ops, self.input_slots, self.output_slots, self.op_info = [], [], {}, []
+        self._ksplit_ops = []  # (op index, workspace bytes) of the split-K convs
         self.conv_flops = 0
         cascades = self._pool_cascades()
         for c in cascades.values():
@@ -673,6 +676,11 @@ class Engine:
                 raise AssertionError(k)
         self.n_ops = len(ops)
         self.ops = (L.Op * max(1, self.n_ops))(*ops)
+        # one fp32 workspace for every split-K conv of the plan (they run in turn on its stream)
+        nws = max([b for _, b in self._ksplit_ops], default=0)
+        self.workspace = torch.empty(max(1, nws // 4), dtype=torch.float32, device=dev) if nws else None
+        for i, _ in self._ksplit_ops:
+            self.ops[i].workspace = self.workspace.data_ptr()
         self.head_params = []
         self.head_unstored = set()  # fused head ops that do not store raw logits (enable_head_decode)
         self.fixed_outputs = None
@@ -779,8 +787,17 @@ class Engine:
                     tile = d.tile = t
                     break
         name = 'stem' if stem else L.lib.ycx_conv_tile_name(tile).decode()
+        if tile == 16 and d.stride == 2 and d.kh == 3 and d.kw == 3 and d.cin == 128 and pool is None:
+            name += '+kcm'  # its own template instance (launch_glds: chunk-major K order), a row of its own in rocprof
+        if not stem and pool is None and not _NO_KSPLIT:
+            ks = int(L.lib.ycx_conv_pick_ksplit(ctypes.byref(d)))
+            if ks > 1:  # split-K (r06): fp32 partials in the plan's workspace, then the ordered reduce launch
+                d.k_split = ks
+                self._ksplit_ops.append((len(self.op_info), int(L.lib.ycx_conv_workspace_size(ctypes.byref(d)))))
+                name += f'+splitk{ks}'
         if pool is not None:
             name += '+maxpool_k2s2'
+        op.d.conv = d  # ctypes copies a struct on assignment: store the final descriptor (tile map, k_split)
         kw = dict(stem=stem, pooled=pool is not None, residual=r is not None)
         nbytes = self._conv_bytes(d, wt, **kw)
         self.op_info.append(dict(kind=node.kind, name=name, flops=flops, shape=shape, parts=node.p.get('parts', 1),

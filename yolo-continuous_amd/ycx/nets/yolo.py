@@ -212,11 +212,12 @@ class Model(nn.Module):
             # re-plan in bf16 (fp32's exponent range, 8-bit significand) for this and every later call.
             import warnings
             if (self.precision,) + tuple(int(v) for v in x.shape[2:]) in self._prepacked:
-                # a bf16 re-plan would fold this module's own parameters, not the prepacked ones
-                warnings.warn("ycx: the fp16 plan overflowed (non-finite head logits) on prepacked weights; "
-                              "returning them as they are (re-pack in 'bf16' or 'f32' for this checkpoint)",
-                              RuntimeWarning, stacklevel=2)
-                return outs
+                # a bf16 re-plan would fold this module's own parameters, not the prepacked ones: raise
+                # (as Detector.check does) rather than hand inf / NaN heads to a serving caller
+                from .. import _lib
+                raise _lib.YcxRangeError("ycx: the fp16 plan produced non-finite head logits on prepacked "
+                                         "weights (an activation exceeds 65504); re-pack this checkpoint in "
+                                         "'bf16' or 'f32'")
             warnings.warn("ycx: the fp16 plan overflowed (non-finite head logits: an activation exceeds "
                           "65504); switching this Model to precision='bf16' (about 1e-3 relative error, "
                           "use 'f32' for the 1e-3 parity mode)", RuntimeWarning, stacklevel=2)
