@@ -43,7 +43,8 @@ def test_abi_metadata_without_gpu():
     assert _lib.lib.ycx_conv_tile_name(50) == b"halo3x3s2_wsr_co128"
     assert _lib.lib.ycx_conv_tile_name(55) == b"wres1x1_pair"
     assert _lib.lib.ycx_conv_tile_name(56) == b"glds_co64_px128_k64_s3"
-    assert _lib.lib.ycx_conv_tile_name(57) == b"invalid"
+    assert _lib.lib.ycx_conv_tile_name(57) == b"retired_wsp_co128_px128_k64_ns4"
+    assert _lib.lib.ycx_conv_tile_name(58) == b"invalid"
     # argument validation happens before any device call
     assert _lib.lib.ycx_conv2d(None, None, None, None, None, None, None) == _lib.YCX_ERR_BAD_ARG
     assert _lib.lib.ycx_sort_nms(None, None, None, None, None, 0, None, None, None, None) == _lib.YCX_ERR_BAD_ARG

@@ -164,12 +164,12 @@ def test_conv_splitk_rejects(device):
                       L.DT_F32 if tile == 8 else L.DT_BF16, k_split=2)
 
 
-@pytest.mark.parametrize('tile', [27, 31, 33, 40, 41, 42, 43, 44, 47])
+@pytest.mark.parametrize('tile', [27, 31, 33, 40, 41, 42, 43, 44, 47, 57])
 def test_retired_tiles_are_not_dispatched(device, tile):
     """Tiles 27-33 (rejected experiments) exist only in a
     -DYCX_EXPERIMENTAL_TILES build; tiles 40-47 (conv_bigt, r03) only with
-    tools/experiments/conv_bigt_tiles40_47.patch applied: the product library
-    refuses them."""
+    tools/experiments/conv_bigt_tiles40_47.patch applied, tile 57 (warp-specialised,
+    r06) only with tools/experiments/wsp_tile57.patch: the product library refuses them."""
     with pytest.raises(L.YcxError, match='unsupported'):
         _run_conv(device, 2, 13, 11, 64, 128, 3, 1, L.ACT_SILU, tile, L.DT_BF16)
 

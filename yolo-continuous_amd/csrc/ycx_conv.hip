@@ -3332,6 +3332,7 @@ const TileInfo kTiles[] = {
     {128, 256, 64, "retired_glds16w_co128_px256_s3"},
     {256, 64, 64, "wres1x1_pair"},  // 55: ycx_conv2d_pair only (two chained 1x1 convs)
     {64, 128, 64, "glds_co64_px128_k64_s3"},  // 56: tile 18 with a three-stage ring (r06)
+    {128, 128, 64, "retired_wsp_co128_px128_k64_ns4"},  // 57: tools/experiments/wsp_tile57.patch (r06)
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
