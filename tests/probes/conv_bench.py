@@ -42,7 +42,7 @@ SHAPES = [  # n, h, w, cin, cout, k, s
     (32, 20, 20, 512, 1024, 3, 1),
     (32, 40, 40, 256, 512, 3, 1),
 ]
-# CONV_ACT=0|1|2: the activation (default SiLU). CONV_EXTRA="64,32,32,4096,4096,1,1;32,40,40,1024,1024,1,1": extra shapes appended (indices continue)
+# CONV_ACT=0|1|2: the activation (default SiLU). CONV_DT=fp16: IEEE half elements (default bf16). CONV_EXTRA="64,32,32,4096,4096,1,1;32,40,40,1024,1024,1,1": extra shapes appended (indices continue)
 for _s in filter(None, os.environ.get("CONV_EXTRA", "").split(";")):
     SHAPES.append(tuple(int(v) for v in _s.split(",")))
 
@@ -57,15 +57,16 @@ def run(shape, tile, iters=20):
         cpad = -(-cout // 256) * 256
     if tile in (1, 4, 7, 9, 12, 14, 16, 20, 21, 26, 28, 31, 32, 42, 43, 49) and cpad % 128:
         return None
-    x = torch.randn(n, h, w, cin, device=dev).to(torch.bfloat16)
-    wt = (torch.randn(cpad, k * k * cin, device=dev) * 0.05).to(torch.bfloat16)
+    tdt, ldt = (torch.float16, L.DT_F16) if os.environ.get("CONV_DT") == "fp16" else (torch.bfloat16, L.DT_BF16)
+    x = torch.randn(n, h, w, cin, device=dev).to(tdt)
+    wt = (torch.randn(cpad, k * k * cin, device=dev) * 0.05).to(tdt)
     b = torch.zeros(cpad, device=dev)
-    y = torch.empty(n, ho, wo, cout, device=dev, dtype=torch.bfloat16)
+    y = torch.empty(n, ho, wo, cout, device=dev, dtype=tdt)
     d = L.ConvDesc()
     d.n, d.h, d.w, d.cin, d.in_c_off, d.in_c_stride = n, h, w, cin, 0, cin
     d.ho, d.wo, d.cout, d.cout_pad, d.out_c_off, d.out_c_stride = ho, wo, cout, cpad, 0, cout
     d.kh = d.kw = k
-    d.stride, d.pad, d.act, d.dtype, d.out_layout, d.tile = s, p, int(os.environ.get("CONV_ACT", L.ACT_SILU)), L.DT_BF16, L.OUT_NHWC, tile
+    d.stride, d.pad, d.act, d.dtype, d.out_layout, d.tile = s, p, int(os.environ.get("CONV_ACT", L.ACT_SILU)), ldt, L.OUT_NHWC, tile
     st = L.stream_handle(dev)
     args = (ctypes.byref(d), x.data_ptr(), wt.data_ptr(), b.data_ptr(), y.data_ptr(), None, st)
     rc = L.lib.ycx_conv2d(*args)
