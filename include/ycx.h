@@ -62,7 +62,12 @@ enum {
  * that holds north_star's 1e-3 at bf16 speed. Activations must stay below
  * 65504 in magnitude (fp16 range). */
 enum { YCX_DT_BF16 = 0, YCX_DT_F32 = 1, YCX_DT_FP8 = 2, YCX_DT_F16 = 3 };
-enum { YCX_ACT_NONE = 0, YCX_ACT_SILU = 1, YCX_ACT_LEAKY = 2 };
+/* YCX_ACT_SILU_PS: SiLU of a conv whose packed weights and bias were pre-multiplied by
+ * k = -log2(e) (fp8: the fp32 bias and dequantisation rows instead), so the epilogue holds
+ * c' = k c and computes silu(c) = c' / (k (1 + 2^c')) = c' * rcp(fma(2^c', k, k)) -- one
+ * exp, one fma, one rcp and one multiply per value instead of a multiply more (r06). The
+ * 16-bit and fp8 kernels; not the fp32 parity path. */
+enum { YCX_ACT_NONE = 0, YCX_ACT_SILU = 1, YCX_ACT_LEAKY = 2, YCX_ACT_SILU_PS = 3 };
 enum {
   YCX_OUT_NHWC = 0,       /* activation dtype, [N][Ho][Wo][out_c_stride] at out_c_off         */
   YCX_OUT_NCHW_F32 = 1,   /* fp32 [N][out_c_stride][Ho][Wo] at out_c_off (Detect raw logits)   */

@@ -14,7 +14,7 @@ L = pytest.importorskip("ycx._lib")
 
 def _ref_conv(x_nchw, w, b, s, p, act, slope=0.1):
     y = F.conv2d(x_nchw.double(), w.double(), b.double(), s, p)
-    if act == L.ACT_SILU:
+    if act in (L.ACT_SILU, L.ACT_SILU_PS):
         y = F.silu(y)
     elif act == L.ACT_LEAKY:
         y = F.leaky_relu(y, slope)
@@ -31,10 +31,11 @@ def _run_conv(device, n, h, w, cin, cout, k, s, act, tile, dtype, in_extra=0, ou
     wt = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to(tdt)
     b = torch.randn(cout, generator=g) * 0.1
     cpad = -(-cout // 64) * 64 if dtype == L.DT_F32 else (32 if cout <= 32 else 64 if cout <= 64 else -(-cout // 128) * 128)
+    ks = L.SILU_PS_K if act == L.ACT_SILU_PS else 1.0  # YCX_ACT_SILU_PS: weights and bias packed x -log2(e)
     wp = torch.zeros(cpad, k, k, cin, dtype=tdt)
-    wp[:cout] = wt.permute(0, 2, 3, 1)
+    wp[:cout] = (wt.double() * ks).to(tdt).permute(0, 2, 3, 1)
     bp = torch.zeros(cpad)
-    bp[:cout] = b
+    bp[:cout] = b * ks
     up = 2 if layout == L.OUT_NHWC_UP2 else 1
     if layout == L.OUT_NCHW_F32:
         y = torch.zeros(n, cout, ho, wo, dtype=torch.float32)
@@ -141,6 +142,28 @@ def test_conv_splitk_residual_up2(device, dtype, layout, residual, act, tile):
                          layout == L.OUT_NHWC else 0, residual=residual, layout=layout, k_split=2)
     tol = 1e-2 if dtype == L.DT_BF16 else 2e-3
     torch.testing.assert_close(got, ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize('tile,cout,cin,k,s', [(16, 128, 64, 3, 1), (18, 64, 128, 3, 2), (16, 128, 128, 3, 2),
+                                               (22, 256, 256, 1, 1), (22, 128, 128, 1, 1), (23, 64, 64, 3, 1),
+                                               (20, 128, 64, 3, 1), (50, 128, 64, 3, 2), (5, 32, 32, 3, 1),
+                                               (7, 128, 32, 3, 1), (17, 64, 32, 3, 1)])
+@pytest.mark.parametrize('dtype', [L.DT_BF16, L.DT_F16])
+def test_conv_silu_prescaled(device, tile, cout, cin, k, s, dtype):
+    """YCX_ACT_SILU_PS (r06): weights and bias packed x -log2(e), the epilogue's SiLU one multiply
+    shorter; against torch's silu of the unscaled conv on the same operands, every tile family
+    (LDS-DMA, register-staged, weight-resident 1x1, weight-stationary 3x3, halo, tile 50)."""
+    h, w = (32, 32) if tile in (23, 20, 50) else (13, 11)
+    got, ref = _run_conv(device, 2, h, w, cin, cout, k, s, L.ACT_SILU_PS, tile, dtype, in_extra=0 if tile in (22, 23, 50) else 8,
+                         out_extra=0 if tile in (22, 23, 50) else 16)
+    tol = 1e-2 if dtype == L.DT_BF16 else 2e-3
+    torch.testing.assert_close(got, ref, rtol=tol, atol=tol)
+
+
+def test_conv_silu_prescaled_rejects_f32(device):
+    """The fp32 parity path keeps torch's silu: YCX_ACT_SILU_PS is refused there."""
+    with pytest.raises(L.YcxError, match='unsupported'):
+        _run_conv(device, 2, 13, 11, 64, 128, 3, 1, L.ACT_SILU_PS, 8, L.DT_F32)
 
 
 def test_conv_splitk_rejects(device):
@@ -488,7 +511,9 @@ def test_stem(device, cin, k, s, dtype, h, w, cout):
                                                  (2, 32, L.ACT_SILU, (2, 64, 128)),
                                                  (1, 64, L.ACT_SILU, (3, 256, 512)),    # 3 tiles per block
                                                  (1, 64, L.ACT_SILU, (5, 128, 256)),    # ragged: 1-2 per block
-                                                 (2, 64, L.ACT_LEAKY, (3, 512, 512))])  # ragged, stem stride 2
+                                                 (2, 64, L.ACT_LEAKY, (3, 512, 512)),   # ragged, stem stride 2
+                                                 (1, 64, L.ACT_SILU_PS, (3, 256, 512)),  # pre-scaled SiLU (r06)
+                                                 (2, 48, L.ACT_SILU_PS, (2, 64, 128))])
 def test_stem_conv2_fused(device, stem_s, cout, act, nhw):
     """ycx_stem_conv2 = stem (3x3, 3->32) then 3x3/s2 conv, stem map kept in LDS
     (rounded to bf16 there, as the unfused path stores it); the larger shapes give each
@@ -513,12 +538,13 @@ def test_stem_conv2_fused(device, stem_s, cout, act, nhw):
     dc.ho, dc.wo, dc.cout, dc.cout_pad, dc.out_c_off, dc.out_c_stride = ho, wo, cout, 64, out_extra, cout + out_extra
     dc.kh = dc.kw = 3
     dc.stride, dc.pad, dc.act, dc.leaky_slope, dc.dtype, dc.out_layout = 2, 1, act, 0.1, L.DT_BF16, L.OUT_NHWC
-    wsp = ws.permute(2, 3, 1, 0).contiguous()                      # [kh][kw][cin][cout_pad] fp32
+    ks = L.SILU_PS_K if act == L.ACT_SILU_PS else 1.0  # YCX_ACT_SILU_PS: both layers packed x -log2(e)
+    wsp = (ws.double() * ks).float().permute(2, 3, 1, 0).contiguous()  # [kh][kw][cin][cout_pad] fp32
     wcp = torch.zeros(64, 3, 3, 32, dtype=torch.bfloat16)
-    wcp[:cout] = wc.permute(0, 2, 3, 1)
+    wcp[:cout] = (wc.double() * ks).to(torch.bfloat16).permute(0, 2, 3, 1)
     bcp = torch.zeros(64)
-    bcp[:cout] = bc
-    t = [v.to(device) for v in (x, wsp, bs, wcp, bcp, y)]
+    bcp[:cout] = bc * ks
+    t = [v.to(device) for v in (x, wsp, (bs.double() * ks).float(), wcp, bcp, y)]
     L.check(L.lib.ycx_stem_conv2(ctypes.byref(ds), ctypes.byref(dc), *[v.data_ptr() for v in t],
                                  L.stream_handle(device)))
     torch.cuda.synchronize()

@@ -3,7 +3,7 @@
 # each arm: A = yolo-continuous_amd/ycx/libycx_A.so (or A_ENV="VAR=value" on the in-tree library),
 # B = the in-tree library. Run through gpurun:  bash tools/ab_trace.sh r06 [bench args]
 # 1. the bench, A B A B (--cpu-seconds 0 --fp16-steps 0 --image-in-steps 0), per-op tables of both arms
-# 2. per arm: rocprofv3 --kernel-trace of the bench's timed loop -> tools/trace_busy.py
+# 2. per arm (unless NO_TRACE=1): rocprofv3 --kernel-trace of the bench's timed loop -> tools/trace_busy.py
 R=${1:-r06}; shift
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$ROOT/gpurun_out/$R/ab
@@ -23,6 +23,7 @@ for v in A B A B; do
   YCX_BENCH_KERNELS=$O/ops_$v.json timeout -k 10 300 python "$ROOT/bench.py" $FAST "$@" > "$O/bench_$v.log" 2>&1 || { tail -5 "$O/bench_$v.log"; exit 1; }
   tail -1 "$O/bench_$v.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', d['value'], d['ms_per_step'], d['p50_ms'], d['roofline']['forward_kernel_ms'])"
 done
+[ -n "$NO_TRACE" ] && exit 0
 cd /tmp && export TMPDIR=/tmp
 for v in A B; do
   arm $v

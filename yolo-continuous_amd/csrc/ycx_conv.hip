@@ -391,6 +391,15 @@ __device__ __forceinline__ f32x4 act4_t(f32x4 v, float slope, float nl2e) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) d[q] = __builtin_amdgcn_rcpf(d[q]);
     return v * d;
+  } else if constexpr (ACT == YCX_ACT_SILU_PS) {  // v = k c with k = nl2e (pre-scaled weights): c / (1 + 2^v)
+    f32x4 d;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = __builtin_amdgcn_exp2f(v[q]);
+    const f32x4 kk = f32x4{nl2e, nl2e, nl2e, nl2e};
+    d = __builtin_elementwise_fma(d, kk, kk);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = __builtin_amdgcn_rcpf(d[q]);
+    return v * d;
   } else {
     f32x4 r;
 #pragma unroll
@@ -401,6 +410,7 @@ __device__ __forceinline__ f32x4 act4_t(f32x4 v, float slope, float nl2e) {
 
 // act4_t with the act code at run time (one uniform branch per call)
 __device__ __forceinline__ f32x4 act4(f32x4 v, int act, float slope, float nl2e) {
+  if (act == YCX_ACT_SILU_PS) return act4_t<YCX_ACT_SILU_PS>(v, slope, nl2e);
   if (act == YCX_ACT_SILU) return act4_t<YCX_ACT_SILU>(v, slope, nl2e);
   if (act == YCX_ACT_LEAKY) return act4_t<YCX_ACT_LEAKY>(v, slope, nl2e);
   return v;
@@ -3358,6 +3368,7 @@ ycx_status launch_ws64(ConvArgs a, hipStream_t st) {
   const long long ntiles = (long long)a.N * (a.Ho / 16) * (a.Wo / 16);
   const dim3 g((unsigned)std::min<long long>(ntiles, 256)), b(512);
   switch (a.act) {
+    case YCX_ACT_SILU_PS: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_SILU_PS>), g, b, 0, st, a); break;
     case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_SILU>), g, b, 0, st, a); break;
     case YCX_ACT_LEAKY: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_LEAKY>), g, b, 0, st, a); break;
     default: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_NONE>), g, b, 0, st, a); break;
@@ -3380,6 +3391,7 @@ ycx_status launch_s2wsr(ConvArgs a, hipStream_t st) {
   const long long ntiles = (long long)a.N * (a.Ho / 4) * (a.Wo / 16);
   const dim3 g((unsigned)std::min<long long>(ntiles, 256)), b(512);
   switch (a.act) {
+    case YCX_ACT_SILU_PS: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_SILU_PS, 4, YCX_S2WSR_NB>), g, b, 0, st, a); break;
     case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_SILU, 4, YCX_S2WSR_NB>), g, b, 0, st, a); break;
     case YCX_ACT_LEAKY: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_LEAKY, 4, YCX_S2WSR_NB>), g, b, 0, st, a); break;
     default: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_NONE, 4, YCX_S2WSR_NB>), g, b, 0, st, a); break;
@@ -3439,6 +3451,7 @@ ycx_status launch_glds(ConvArgs a, hipStream_t st) {
       const long long total = (long long)a.M * (a.Cout >> 3);
       const dim3 rg((unsigned)std::min<long long>((total + 255) / 256, 4096)), rb(256);
       switch (a.act) {
+        case YCX_ACT_SILU_PS: hipLaunchKernelGGL(splitk_reduce<YCX_ACT_SILU_PS>, rg, rb, 0, st, a); break;
         case YCX_ACT_SILU: hipLaunchKernelGGL(splitk_reduce<YCX_ACT_SILU>, rg, rb, 0, st, a); break;
         case YCX_ACT_LEAKY: hipLaunchKernelGGL(splitk_reduce<YCX_ACT_LEAKY>, rg, rb, 0, st, a); break;
         default: hipLaunchKernelGGL(splitk_reduce<YCX_ACT_NONE>, rg, rb, 0, st, a); break;
@@ -3525,6 +3538,7 @@ ycx_status launch_wres_k(ConvArgs a, hipStream_t st) {
   a.nwg = R * a.n_ct;
   dim3 g(a.nwg), b(WCO * WPX * 64);
   switch (a.act) {
+    case YCX_ACT_SILU_PS: return launch_wres_cin<WCO, WPX, TPW, NS, SUB, YCX_ACT_SILU_PS>(a, g, b, st);
     case YCX_ACT_SILU: return launch_wres_cin<WCO, WPX, TPW, NS, SUB, YCX_ACT_SILU>(a, g, b, st);
     case YCX_ACT_LEAKY: return launch_wres_cin<WCO, WPX, TPW, NS, SUB, YCX_ACT_LEAKY>(a, g, b, st);
     default: return launch_wres_cin<WCO, WPX, TPW, NS, SUB, YCX_ACT_NONE>(a, g, b, st);
@@ -3600,6 +3614,7 @@ ycx_status launch_wres_f8_k(ConvArgs a, hipStream_t st) {
   a.nwg = R * a.n_ct;
   dim3 g(a.nwg), b(WCO * WPX * 64);
   switch (a.act) {
+    case YCX_ACT_SILU_PS: return launch_wres_f8_cin<WCO, WPX, TPW, NS, YCX_ACT_SILU_PS>(a, g, b, st);
     case YCX_ACT_SILU: return launch_wres_f8_cin<WCO, WPX, TPW, NS, YCX_ACT_SILU>(a, g, b, st);
     case YCX_ACT_LEAKY: return launch_wres_f8_cin<WCO, WPX, TPW, NS, YCX_ACT_LEAKY>(a, g, b, st);
     default: return launch_wres_f8_cin<WCO, WPX, TPW, NS, YCX_ACT_NONE>(a, g, b, st);
@@ -3615,6 +3630,7 @@ ycx_status launch_ws64_f8(ConvArgs a, hipStream_t st) {
   const long long ntiles = (long long)a.N * (a.Ho / 16) * (a.Wo / 16);
   const dim3 g((unsigned)std::min<long long>(ntiles, 256)), b(512);
   switch (a.act) {
+    case YCX_ACT_SILU_PS: hipLaunchKernelGGL((conv3x3_ws64_f8<YCX_ACT_SILU_PS>), g, b, 0, st, a); break;
     case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3_ws64_f8<YCX_ACT_SILU>), g, b, 0, st, a); break;
     case YCX_ACT_LEAKY: hipLaunchKernelGGL((conv3x3_ws64_f8<YCX_ACT_LEAKY>), g, b, 0, st, a); break;
     default: hipLaunchKernelGGL((conv3x3_ws64_f8<YCX_ACT_NONE>), g, b, 0, st, a); break;
@@ -3821,7 +3837,8 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d_ws)(const ycx_conv_desc* d, const void*
   YCX_CHECK_ARG(d->out_layout == YCX_OUT_NCHW_F32 || d->out_c_off + d->cout <= d->out_c_stride);
   YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_ELT || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
   YCX_CHECK_SUPPORTED(d->out_layout >= YCX_OUT_NHWC && d->out_layout <= YCX_OUT_NHWC_UP2);
-  YCX_CHECK_SUPPORTED(d->act >= YCX_ACT_NONE && d->act <= YCX_ACT_LEAKY);
+  YCX_CHECK_SUPPORTED(d->act >= YCX_ACT_NONE && d->act <= YCX_ACT_SILU_PS);
+  YCX_CHECK_SUPPORTED(d->act != YCX_ACT_SILU_PS || d->dtype != YCX_DT_F32);  // fp32 parity mode: plain SiLU
   YCX_CHECK_SUPPORTED(!residual || d->out_layout == YCX_OUT_NHWC);
   const int vec = d->dtype == YCX_DT_ELT ? 8 : d->dtype == YCX_DT_FP8 ? 16 : 4;  // 16-byte DMA chunks
   YCX_CHECK_SUPPORTED(d->in_c_off % vec == 0 && d->in_c_stride % vec == 0);
@@ -3948,7 +3965,7 @@ extern "C" ycx_status YCX_SFX(ycx_conv2d_pair)(const ycx_conv_desc* da, const yc
   YCX_CHECK_SUPPORTED(da->dtype == YCX_DT_ELT && db->dtype == YCX_DT_ELT);
   for (const ycx_conv_desc* d : {da, db}) {
     YCX_CHECK_SUPPORTED(d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && !d->in_pool &&
-                        d->out_layout == YCX_OUT_NHWC && d->act >= YCX_ACT_NONE && d->act <= YCX_ACT_LEAKY);
+                        d->out_layout == YCX_OUT_NHWC && d->act >= YCX_ACT_NONE && d->act <= YCX_ACT_SILU_PS);
     YCX_CHECK_SUPPORTED(d->out_c_off % 8 == 0 && d->out_c_stride % 8 == 0);
   }
   YCX_CHECK_SUPPORTED((da->cin == 64 || da->cin == 128 || da->cin == 256) && da->cout == 256 && da->cout_pad == 256);
@@ -3973,6 +3990,8 @@ extern "C" ycx_status YCX_SFX(ycx_stem_conv)(const ycx_conv_desc* d, const float
   YCX_CHECK_SUPPORTED(d->out_layout == YCX_OUT_NHWC || d->out_layout == YCX_OUT_NHWC_UP2);
   YCX_CHECK_SUPPORTED(d->dtype == YCX_DT_ELT || d->dtype == YCX_DT_F32 || d->dtype == YCX_DT_FP8);
   YCX_CHECK_SUPPORTED((long long)d->n * d->ho * d->wo < (1LL << 31) && !d->in_pool);
+  YCX_CHECK_SUPPORTED(d->act >= YCX_ACT_NONE && d->act <= YCX_ACT_SILU_PS &&
+                      (d->act != YCX_ACT_SILU_PS || d->dtype != YCX_DT_F32));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ConvArgs a = make_args(d, x, w, bias, y, nullptr);
   a.Ktot = d->kh * d->kw * d->cin;  // fp32 stem weights: no fp8 row padding
@@ -4042,8 +4061,8 @@ extern "C" ycx_status YCX_SFX(ycx_stem_conv2)(const ycx_conv_desc* sd, const ycx
   // FP8: the pair computes in bf16 (the stem map never leaves LDS); the output is e4m3 (cd->out_scale)
   YCX_CHECK_SUPPORTED(sd->dtype == cd->dtype && (cd->dtype == YCX_DT_ELT || cd->dtype == YCX_DT_FP8) &&
                       cd->out_layout == YCX_OUT_NHWC);
-  YCX_CHECK_SUPPORTED(sd->act >= YCX_ACT_NONE && sd->act <= YCX_ACT_LEAKY && cd->act >= YCX_ACT_NONE &&
-                      cd->act <= YCX_ACT_LEAKY);
+  YCX_CHECK_SUPPORTED(sd->act >= YCX_ACT_NONE && sd->act <= YCX_ACT_SILU_PS && cd->act >= YCX_ACT_NONE &&
+                      cd->act <= YCX_ACT_SILU_PS);
   YCX_CHECK_SUPPORTED(cd->ho % kS2TH == 0 && cd->wo % kS2TW == 0);
   YCX_CHECK_SUPPORTED((long long)cd->n * cd->ho * cd->wo < (1LL << 31));
   ConvArgs sa = make_args(sd, x, w_stem, b_stem, nullptr, nullptr);
@@ -4064,9 +4083,11 @@ extern "C" ycx_status YCX_SFX(ycx_stem_conv2)(const ycx_conv_desc* sd, const ycx
       hipLaunchKernelGGL((stem2_fused<SS_, A1_, A2_>), g, b, 0, st, sa, ca);              \
     return ycx_launch_status();                                                           \
   }
+  YCX_STEM2(1, YCX_ACT_SILU_PS, YCX_ACT_SILU_PS)
   YCX_STEM2(1, YCX_ACT_SILU, YCX_ACT_SILU)
   YCX_STEM2(1, YCX_ACT_LEAKY, YCX_ACT_LEAKY)
   YCX_STEM2(1, YCX_ACT_NONE, YCX_ACT_NONE)
+  YCX_STEM2(2, YCX_ACT_SILU_PS, YCX_ACT_SILU_PS)
   YCX_STEM2(2, YCX_ACT_SILU, YCX_ACT_SILU)
   YCX_STEM2(2, YCX_ACT_LEAKY, YCX_ACT_LEAKY)
   YCX_STEM2(2, YCX_ACT_NONE, YCX_ACT_NONE)

@@ -66,6 +66,8 @@ __device__ __forceinline__ float ycx_act(float v, int act, float slope) {
     return FAST ? v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.44269504f))
                 : v / (1.0f + expf(-v));
   if (act == YCX_ACT_LEAKY) return v > 0.0f ? v : v * slope;
+  if (act == YCX_ACT_SILU_PS)  // v = -log2(e) c (pre-scaled weights): c / (1 + 2^v)
+    return v * __builtin_amdgcn_rcpf(__builtin_fmaf(__builtin_amdgcn_exp2f(v), -1.44269504f, -1.44269504f));
   return v;
 }
 
@@ -74,6 +76,8 @@ template <int ACT>
 __device__ __forceinline__ float act_t(float v, float slope) {
   if constexpr (ACT == YCX_ACT_SILU) return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.44269504f));
   else if constexpr (ACT == YCX_ACT_LEAKY) return v > 0.0f ? v : v * slope;
+  else if constexpr (ACT == YCX_ACT_SILU_PS)
+    return v * __builtin_amdgcn_rcpf(__builtin_fmaf(__builtin_amdgcn_exp2f(v), -1.44269504f, -1.44269504f));
   else return v;
 }
 

@@ -23,7 +23,8 @@ ABI_VERSION = 9
 # ---- enums (ycx.h) ----
 YCX_OK, YCX_ERR_BAD_ARG, YCX_ERR_UNSUPPORTED, YCX_ERR_LAUNCH, YCX_ERR_CAPACITY = 0, 1, 2, 3, 4
 DT_BF16, DT_F32, DT_FP8, DT_F16 = 0, 1, 2, 3
-ACT_NONE, ACT_SILU, ACT_LEAKY = 0, 1, 2
+ACT_NONE, ACT_SILU, ACT_LEAKY, ACT_SILU_PS = 0, 1, 2, 3
+SILU_PS_K = -1.4426950408889634  # -log2(e): the pre-scale of YCX_ACT_SILU_PS weights and bias (ycx.h)
 OUT_NHWC, OUT_NCHW_F32, OUT_NHWC_UP2 = 0, 1, 2
 OP_CONV, OP_STEM, OP_POOL, OP_COPY, OP_STEM2, OP_HEAD, OP_CONV_PAIR = 1, 2, 3, 4, 5, 6, 7
 

@@ -273,6 +273,8 @@ _TILE_MAP = {int(a): [int(t) for t in b.split('/')] for a, b in
              (kv.split(':') for kv in os.environ.get('YCX_TILE_MAP', '').split(',') if kv)}
 # A/B switch: YCX_NO_KSPLIT=1 runs every conv unsplit even where ycx_conv_pick_ksplit splits its K loop
 _NO_KSPLIT = bool(os.environ.get('YCX_NO_KSPLIT'))
+# A/B switch: YCX_NO_SILU_PS=1 packs SiLU convs unscaled and runs the plain YCX_ACT_SILU epilogue
+_NO_SILU_PS = bool(os.environ.get('YCX_NO_SILU_PS'))
 
 
 def cascade_fits(h, w, c, esz):
@@ -716,6 +718,10 @@ class Engine:
         else:     # [cout_pad][kh][kw][cin] in the activation dtype
             wshape, wdt = (cpad, k, k, cin), self.dtype
         bshape = (2 * cpad,) if (f8 and not stem and not bf16_weights) else (cpad,)
+        # SiLU epilogues of the 16-bit / fp8 plans run on c' = -log2(e) c (YCX_ACT_SILU_PS): the weights
+        # and bias are scaled here in float64 before their one rounding (fp8: the fp32 bias and dq rows,
+        # so the e4m3 weights are unchanged); the fp32 parity plan keeps torch's silu(c) = c / (1 + e^-c)
+        silu_ps = p['act'] == L.ACT_SILU and self.dt != L.DT_F32 and not _NO_SILU_PS
         i = 2 * self._conv_index[id(node)]
         if self.prepacked is not None:
             wt, bt = self.prepacked.get(f"p{i}"), self.prepacked.get(f"p{i + 1}")
@@ -727,13 +733,16 @@ class Engine:
             wp[:cout] = w64
             bp = torch.zeros(cpad, dtype=torch.float64)
             bp[:cout] = b64
+            ks = L.SILU_PS_K if silu_ps else 1.0
+            if not (f8 and not stem and not bf16_weights):
+                wp, bp = wp * ks, bp * ks
             if stem:
                 wt = wp.permute(2, 3, 1, 0).contiguous().to(torch.float32)
             elif bf16_weights:
                 wt = wp.permute(0, 2, 3, 1).contiguous().to(wdt)
             elif f8:
                 wt, sw = pack_fp8_weights(wp)
-                bp = torch.cat([bp, 1.0 / (sw * self._scale(x))])  # dq[co] = 1 / (s_w[co] s_x)
+                bp = torch.cat([bp * ks, ks / (sw * self._scale(x))])  # dq[co] = 1 / (s_w[co] s_x), both x ks
             else:
                 wt = wp.permute(0, 2, 3, 1).contiguous().to(self.dtype)
             bt = bp.to(torch.float32)
@@ -752,7 +761,7 @@ class Engine:
             d.in_c_off, d.in_c_stride, d.in_pool = src.coff, src.buf.c, 1
         d.ho, d.wo, d.cout, d.cout_pad = p['ho'], p['wo'], cout, cpad
         d.kh = d.kw = k
-        d.stride, d.pad, d.act, d.leaky_slope = p['s'], p['p'], p['act'], p['slope']
+        d.stride, d.pad, d.act, d.leaky_slope = p['s'], p['p'], (L.ACT_SILU_PS if silu_ps else p['act']), p['slope']
         d.dtype, d.out_layout = self.dt, p['layout']
         if p['layout'] == L.OUT_NCHW_F32:
             d.out_c_off, d.out_c_stride = 0, cout

@@ -29,7 +29,8 @@ import json
 
 import torch
 
-FORMAT = "ycx-prepack-3"  # 3 (r05): tensors named by conv node (2i, 2i+1), independent of which convs fuse
+FORMAT = "ycx-prepack-4"  # 3 (r05): tensors named by conv node (2i, 2i+1), independent of which convs fuse;
+#                            4 (r06): SiLU convs of 16-bit / fp8 plans packed pre-scaled by -log2(e) (YCX_ACT_SILU_PS)
 
 
 def state_dict_sha256(model):
