@@ -23,11 +23,12 @@ def main():
     ds.n, ds.h, ds.w, ds.cin, ds.in_c_off, ds.in_c_stride = n, h, w, 3, 0, 3
     ds.ho, ds.wo, ds.cout, ds.cout_pad, ds.out_c_off, ds.out_c_stride = h, w, 32, 32, 0, 32
     ds.kh = ds.kw = 3
-    ds.stride, ds.pad, ds.act, ds.dtype, ds.out_layout = 1, 1, L.ACT_SILU, L.DT_BF16, L.OUT_NHWC
+    act = int(os.environ.get("STEM2_ACT", L.ACT_SILU_PS))  # the plans run SILU_PS (pre-scaled weights)
+    ds.stride, ds.pad, ds.act, ds.dtype, ds.out_layout = 1, 1, act, L.DT_BF16, L.OUT_NHWC
     dc.n, dc.h, dc.w, dc.cin, dc.in_c_off, dc.in_c_stride = n, h, w, 32, 0, 32
     dc.ho, dc.wo, dc.cout, dc.cout_pad, dc.out_c_off, dc.out_c_stride = 320, 320, 64, 64, 0, 64
     dc.kh = dc.kw = 3
-    dc.stride, dc.pad, dc.act, dc.dtype, dc.out_layout = 2, 1, L.ACT_SILU, L.DT_BF16, L.OUT_NHWC
+    dc.stride, dc.pad, dc.act, dc.dtype, dc.out_layout = 2, 1, act, L.DT_BF16, L.OUT_NHWC
     st = L.stream_handle(dev)
 
     def fused():

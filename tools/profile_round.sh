@@ -1,8 +1,10 @@
 #!/bin/bash
 # Profile this round's bench on the GPU box (run through gpurun), one coherent set from one build:
 #   bash tools/profile_round.sh r04
-# 1. rocprofv3 --kernel-trace --stats of the default bench command; the same run writes the per-op
-#    roofline gap table (YCX_BENCH_KERNELS, HIP events of the serial roofline leg)
+# 1. rocprofv3 --kernel-trace --stats of the bench command (headline leg and its roofline leg; the
+#    fp16 leg and the CPU baseline are left out so that the roofline leg is the trace's last conv work:
+#    the f16 build's kernels carry the same symbol names); the same run writes the per-op roofline gap
+#    table (YCX_BENCH_KERNELS, HIP events of the serial roofline leg)
 # 2. tools/trace_leg_stats.py: the profiler's own per-kernel averages over that roofline leg
 # 3. two PMC passes (FETCH_SIZE, WRITE_SIZE) over tools/pmc_workload.py
 # 4. tools/pmc_traffic.py -> per-op HBM bytes (traffic.json)
@@ -17,7 +19,7 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 YCX_BENCH_KERNELS=$OUT/ops.json timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run \
-  --output-format csv -- python3 "$ROOT/bench.py" > "$OUT/bench_under_rocprof.log" 2>&1
+  --output-format csv -- python3 "$ROOT/bench.py" --fp16-steps 0 --cpu-seconds 0 > "$OUT/bench_under_rocprof.log" 2>&1
 TRACE=$(find "$OUT/trace" -name '*kernel_trace.csv' | head -n 1)
 NOPS=$(python3 -c "import json; print(len(json.load(open('$OUT/ops.json'))['ops']))")
 python3 "$ROOT/tools/trace_leg_stats.py" "$TRACE" "$NOPS" 3 "$OUT/kernel_stats_roofline_leg.csv" > "$OUT/trace_legs.txt"
