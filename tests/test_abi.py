@@ -84,6 +84,11 @@ def test_tile_picker():
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 48  # 40-wide 3x3, 1280 band workgroups
     d.cout_pad = 256
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 16  # 640: too few for the band tile
+    d.h = d.w = d.ho = d.wo = 20
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 16  # 20^2 x bs 32: 200 workgroups (r06)
+    d.n = 4
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 18  # 26: co64 x px128 below 64
+    d.n = 32
     d.dtype = _lib.DT_F32
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 8
 

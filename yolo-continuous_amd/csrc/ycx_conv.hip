@@ -3356,6 +3356,15 @@ ycx_status launch_bf16(ConvArgs a, hipStream_t st) {
   return ycx_launch_status();
 }
 
+// Persistent grids (r06): the fewest blocks that keep a full grid's largest per-block tile count,
+// ceil(T / ceil(T / cap)) for T balanced tiles on at most cap blocks: the same time for this launch,
+// and the CUs it leaves run the other batches in flight (80^2 ws64: 800 tiles, 256 -> 200 blocks).
+inline long long even_grid(long long T, long long cap) {
+  if (T <= cap) return T;
+  const long long per = (T + cap - 1) / cap;
+  return (T + per - 1) / per;
+}
+
 bool ws64_ok(const ConvArgs& a) {
   return a.KH == 3 && a.KW == 3 && a.S == 1 && a.P == 1 && a.H == a.Ho && a.W == a.Wo && a.Ho % 16 == 0 &&
          a.Wo % 16 == 0 && a.Cin == 64 && a.Cout_pad == 64 && a.out_layout == YCX_OUT_NHWC && !a.res &&
@@ -3366,7 +3375,7 @@ bool ws64_ok(const ConvArgs& a) {
 ycx_status launch_ws64(ConvArgs a, hipStream_t st) {
   if (!ws64_ok(a)) return YCX_ERR_UNSUPPORTED;
   const long long ntiles = (long long)a.N * (a.Ho / 16) * (a.Wo / 16);
-  const dim3 g((unsigned)std::min<long long>(ntiles, 256)), b(512);
+  const dim3 g((unsigned)even_grid(ntiles, 256)), b(512);
   switch (a.act) {
     case YCX_ACT_SILU_PS: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_SILU_PS>), g, b, 0, st, a); break;
     case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_SILU>), g, b, 0, st, a); break;
@@ -3389,7 +3398,7 @@ bool s2wsr_ok(const ConvArgs& a) {
 ycx_status launch_s2wsr(ConvArgs a, hipStream_t st) {
   if (!s2wsr_ok(a)) return YCX_ERR_UNSUPPORTED;
   const long long ntiles = (long long)a.N * (a.Ho / 4) * (a.Wo / 16);
-  const dim3 g((unsigned)std::min<long long>(ntiles, 256)), b(512);
+  const dim3 g((unsigned)even_grid(ntiles, 256)), b(512);
   switch (a.act) {
     case YCX_ACT_SILU_PS: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_SILU_PS, 4, YCX_S2WSR_NB>), g, b, 0, st, a); break;
     case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3s2_wsr<YCX_ACT_SILU, 4, YCX_S2WSR_NB>), g, b, 0, st, a); break;
@@ -3534,7 +3543,7 @@ template <int WCO, int WPX, int TPW, int NS, int SUB>
 ycx_status launch_wres_k(ConvArgs a, hipStream_t st) {
   a.n_ct = a.Cout_pad / (WCO * 32);
   const int T = (a.M + TPW * WPX - 1) / (TPW * WPX);
-  const int R = std::max(1, std::min(T, 256 / a.n_ct));
+  const int R = std::max(1, (int)even_grid(T, 256 / a.n_ct));
   a.nwg = R * a.n_ct;
   dim3 g(a.nwg), b(WCO * WPX * 64);
   switch (a.act) {
@@ -3571,7 +3580,7 @@ ycx_status launch_wres(ConvArgs a, hipStream_t st) {
 template <int KC, int NS, int SUB>
 ycx_status launch_wres_pair_k(ConvArgs a, ConvArgs b, hipStream_t st) {
   const int T = (a.M + 63) / 64;
-  a.nwg = std::max(1, std::min(T, 256));
+  a.nwg = std::max(1, (int)even_grid(T, 256));
   if (b.Cout_pad == 128)
     hipLaunchKernelGGL((conv1x1_wres_pair<KC, NS, SUB, 128>), dim3(a.nwg), dim3(512), 0, st, a, b);
   else
@@ -3610,7 +3619,7 @@ template <int WCO, int WPX, int TPW, int NS>
 ycx_status launch_wres_f8_k(ConvArgs a, hipStream_t st) {
   a.n_ct = a.Cout_pad / (WCO * 32);
   const int T = (a.M + TPW * WPX - 1) / (TPW * WPX);
-  const int R = std::max(1, std::min(T, 256 / a.n_ct));
+  const int R = std::max(1, (int)even_grid(T, 256 / a.n_ct));
   a.nwg = R * a.n_ct;
   dim3 g(a.nwg), b(WCO * WPX * 64);
   switch (a.act) {
@@ -3628,7 +3637,7 @@ ycx_status launch_ws64_f8(ConvArgs a, hipStream_t st) {
         !a.res && (long long)a.N * a.H * a.W * a.in_cs < (1LL << 31) - 64))
     return YCX_ERR_UNSUPPORTED;
   const long long ntiles = (long long)a.N * (a.Ho / 16) * (a.Wo / 16);
-  const dim3 g((unsigned)std::min<long long>(ntiles, 256)), b(512);
+  const dim3 g((unsigned)even_grid(ntiles, 256)), b(512);
   switch (a.act) {
     case YCX_ACT_SILU_PS: hipLaunchKernelGGL((conv3x3_ws64_f8<YCX_ACT_SILU_PS>), g, b, 0, st, a); break;
     case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3_ws64_f8<YCX_ACT_SILU>), g, b, 0, st, a); break;
@@ -3672,7 +3681,7 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
   if (d->in_pool) {  // the pooled-operand variants of the two-stage LDS-DMA tiles
     const bool big = d->cout_pad % 128 == 0 && (d->cout_pad / 128) * ((M + 127) / 128) >= 256;
     if (d->dtype == YCX_DT_FP8) return big ? 34 : 35;
-    return big ? 16 : 18;
+    return d->cout_pad % 128 == 0 && (d->cout_pad / 128) * ((M + 127) / 128) >= 64 ? 16 : 18;
   }
   if (d->dtype == YCX_DT_FP8) {
     // pointwise layers with cin in {128, 256, 512} and >= 8 pixel tiles per persistent block:
@@ -3742,9 +3751,11 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
       d->ho % 8 == 0 && d->out_layout != YCX_OUT_NCHW_F32 && (long long)(d->cout_pad / 64) * d->n * (d->ho / 8) >= 1280)
     return 48;
   if (d->cout_pad % 128 == 0) {
-    if ((d->cout_pad / 128) * ((M + 127) / 128) >= 256) return 16;
-    // small-M (deep) layers: co64 x px128 LDS-DMA blocks, two per CU (tests/probes/conv_bench.py,
-    // 20^2 x bs 32: 3x3 256->256 0.037 -> 0.027 ms, 512->256 0.068 -> 0.046 ms against co128 x px64)
+    // Tile 16 down to a quarter wave of workgroups (r06): at 20^2 x bs 32 (200 workgroups) it takes
+    // within 1-2 us of tile 18's time with half the workgroups, and the other batches in flight
+    // run in the CU slots it leaves (concurrent bench +1.3 %, profiles/r06/tile_pick/). Below
+    // that (small batches, latency) the co64 x px128 blocks, two per CU.
+    if ((d->cout_pad / 128) * ((M + 127) / 128) >= 64) return 16;
     return 18;
   }
   if ((M + 255) / 256 >= 512) return 15;  // tests/probes/conv_bench.py: 80^2 x bs 32 128->64 3x3 48.7 vs 52.3 us (t18)
@@ -4072,7 +4083,7 @@ extern "C" ycx_status YCX_SFX(ycx_stem_conv2)(const ycx_conv_desc* sd, const ycx
   sa.Ktot = sd->kh * sd->kw * sd->cin;
   ca.Ktot = cd->kh * cd->kw * cd->cin;
   const long long ntiles = (long long)cd->n * (cd->ho / kS2TH) * (cd->wo / kS2TW);
-  ca.nwg = (int)std::min<long long>(ntiles, 2 * 256);  // persistent: two blocks per CU
+  ca.nwg = (int)even_grid(ntiles, 2 * 256);  // persistent: two blocks per CU
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 g(ca.nwg), b(256);
 #define YCX_STEM2(SS_, A1_, A2_)                                                           \

@@ -268,9 +268,15 @@ def lower_module(g: Graph, m, x):
 
 
 # Development A/B of tile choices: YCX_TILE_MAP="16:24/26,18:26" replaces the picked
-# tile 16 by 24 where cout_pad allows, else 26 (never set in the product path).
-_TILE_MAP = {int(a): [int(t) for t in b.split('/')] for a, b in
-             (kv.split(':') for kv in os.environ.get('YCX_TILE_MAP', '').split(',') if kv)}
+# tile 16 by 24 where cout_pad allows, else 26; "16<600:25/26" only where the picked tile
+# launches fewer than 600 workgroups (never set in the product path).
+_TILE_MAP = {}
+_TILE_SHAPE = {15: (64, 256), 16: (128, 128), 18: (64, 128), 24: (256, 256), 25: (256, 128), 26: (128, 256)}
+for _kv in os.environ.get('YCX_TILE_MAP', '').split(','):
+    if _kv:
+        _a, _b = _kv.split(':')
+        _t, _, _cap = _a.partition('<')
+        _TILE_MAP[int(_t)] = (int(_cap) if _cap else 1 << 62, [int(t) for t in _b.split('/')])
 # A/B switch: YCX_NO_KSPLIT=1 runs every conv unsplit even where ycx_conv_pick_ksplit splits its K loop
 _NO_KSPLIT = bool(os.environ.get('YCX_NO_KSPLIT'))
 # A/B switch: YCX_NO_SILU_PS=1 packs SiLU convs unscaled and runs the plain YCX_ACT_SILU epilogue
@@ -791,10 +797,13 @@ class Engine:
         op.residual = r.buf.tensor.data_ptr() if r is not None else None
         tile = 0 if stem else int(L.lib.ycx_conv_pick_tile(ctypes.byref(d)))
         if not stem and tile in _TILE_MAP:  # development A/B only (YCX_TILE_MAP)
-            for t in _TILE_MAP[tile]:
-                if t not in (24, 25) or d.cout_pad % 256 == 0:
-                    tile = d.tile = t
-                    break
+            cap, alts = _TILE_MAP[tile]
+            bm, bn = _TILE_SHAPE.get(tile, (0, 0))
+            if not bm or -(-d.cout_pad // bm) * -(-(d.n * d.ho * d.wo) // bn) < cap:
+                for t in alts:
+                    if (t not in (24, 25) or d.cout_pad % 256 == 0) and (pool is None or t in (16, 18)):
+                        tile = d.tile = t
+                        break
         name = 'stem' if stem else L.lib.ycx_conv_tile_name(tile).decode()
         if tile == 16 and d.stride == 2 and d.kh == 3 and d.kw == 3 and d.cin == 128 and pool is None:
             name += '+kcm'  # its own template instance (launch_glds: chunk-major K order), a row of its own in rocprof
