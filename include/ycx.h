@@ -337,8 +337,10 @@ ycx_status ycx_decode_filter(const ycx_decode_filter_desc* d, const float* const
 /* Device self-check behind the class scan of the decode filters (no reference
  * counterpart): adds to *violations (device uint64, caller-zeroed) the number of
  * adjacent finite-float pairs x < y with sigmoid(x) > sigmoid(y) for the
- * decoders' sigmoid, over every float. The filters' exact class argmax relies
- * on it being 0 (ycx_internal.h, ycx_class_argmax). */
+ * decoders' sigmoid, over every float, plus (r06) the floats m in [-80, 6] at
+ * which sigmoid(m - max(|m|, 1) 2^-12) is not below sigmoid(m). The filters'
+ * exact class argmax relies on it being 0 (ycx_internal.h, ycx_class_argmax and
+ * the fast path of ycx_class_finish). */
 ycx_status ycx_check_sigmoid_monotone(unsigned long long* violations, void* stream);
 size_t ycx_nms_workspace_size(const ycx_nms_desc* d);
 /* Sorts each image's candidates by (class asc, score desc, row asc) — the order

@@ -620,7 +620,12 @@ __device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const fl
         b = 0;
         ycx_class_scan(logit, 1, c, m, pm, b);
       } else {
+#if defined(YCX_HEAD_ABL) && YCX_HEAD_ABL == 2  // development timing only: class 0 alone
+        m = logit(0);
+        b = 0;
+#else
         ycx_class_scan2(logit, h.nc, m, pm, b);
+#endif
       }
     }
     float m2 = -INFINITY, pm2 = -INFINITY;
@@ -640,7 +645,12 @@ __device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const fl
         bi = 0;
       } else {
         ycx_class_merge(m, pm, b, m2, pm2, b2);
+#if defined(YCX_HEAD_ABL) && YCX_HEAD_ABL == 3  // development timing only: finish = one sigmoid
+        best = head_sigmoid(m);
+        bi = b;
+#else
         ycx_class_finish(logit, m, pm, b, best, bi);
+#endif
       }
       const float score = obj * best;
       if (score >= h.conf_thres) {
@@ -660,6 +670,10 @@ __device__ void head_decode_tile(const ConvArgs& a, const HeadArgs& hd, const fl
                       h.row_off + an * HW + cell};
       }
     }
+#if defined(YCX_HEAD_ABL) && YCX_HEAD_ABL == 4  // development timing only: no append
+    if (cd.row == -7) hd.cand[0] = cd;
+    continue;
+#endif
     if (two) {  // one atomic per (block, image) instead of one per (wave, image)
       const int k = n - n0;
       const unsigned long long q0 = __ballot(pass && k == 0), q1 = __ballot(pass && k == 1);
@@ -1059,6 +1073,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_bf16_glds(ConvArgs a, HeadA
     }
     head_flag(hd, bad);
     __syncthreads();
+#if defined(YCX_HEAD_ABL) && YCX_HEAD_ABL == 1  // development timing only: the decode skipped
+    if (px0 < 0)
+#endif
     head_decode_tile<BN>(a, hd, T, HEAD_LDT, px0);
     done = true;
   }
@@ -3375,7 +3392,10 @@ bool ws64_ok(const ConvArgs& a) {
 ycx_status launch_ws64(ConvArgs a, hipStream_t st) {
   if (!ws64_ok(a)) return YCX_ERR_UNSUPPORTED;
   const long long ntiles = (long long)a.N * (a.Ho / 16) * (a.Wo / 16);
-  const dim3 g((unsigned)even_grid(ntiles, 256)), b(512);
+#ifndef YCX_WS64_BLOCKS  // development A/B knob: the persistent grid's block cap
+#define YCX_WS64_BLOCKS 256
+#endif
+  const dim3 g((unsigned)even_grid(ntiles, YCX_WS64_BLOCKS)), b(512);
   switch (a.act) {
     case YCX_ACT_SILU_PS: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_SILU_PS>), g, b, 0, st, a); break;
     case YCX_ACT_SILU: hipLaunchKernelGGL((conv3x3_ws64<YCX_ACT_SILU>), g, b, 0, st, a); break;
@@ -4083,7 +4103,10 @@ extern "C" ycx_status YCX_SFX(ycx_stem_conv2)(const ycx_conv_desc* sd, const ycx
   sa.Ktot = sd->kh * sd->kw * sd->cin;
   ca.Ktot = cd->kh * cd->kw * cd->cin;
   const long long ntiles = (long long)cd->n * (cd->ho / kS2TH) * (cd->wo / kS2TW);
-  ca.nwg = (int)even_grid(ntiles, 2 * 256);  // persistent: two blocks per CU
+#ifndef YCX_STEM2_BLOCKS  // development A/B knob: the persistent grid's block cap
+#define YCX_STEM2_BLOCKS 512
+#endif
+  ca.nwg = (int)even_grid(ntiles, YCX_STEM2_BLOCKS);  // persistent: two blocks per CU
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 g(ca.nwg), b(256);
 #define YCX_STEM2(SS_, A1_, A2_)                                                           \

@@ -416,18 +416,31 @@ __global__ void __launch_bounds__(256) decode_filter4_kernel(DecodeFilterArgs a,
 }  // namespace
 
 namespace {
+// The premise of ycx_class_finish's fast path for one logit m: sigmoid(m - tau) < sigmoid(m)
+// with tau and m - tau as ycx_class_finish forms them (1 = violated).
+__device__ __forceinline__ unsigned sigmoid_gap_bad(float m, float sm) {
+  if (!(m >= kClassFastLo && m <= kClassFastHi)) return 0u;
+  const float tau = fmaxf(fabsf(m), 1.0f) * 0x1p-12f;
+  return ycx_sigmoid(m - tau) < sm ? 0u : 1u;
+}
+
 // Every finite non-negative bit pattern b (and its negative) against b + 1;
-// 256 consecutive patterns per thread, the previous sigmoid carried.
+// 256 consecutive patterns per thread, the previous sigmoid carried. Also the
+// fast-path premise (sigmoid_gap_bad) at every one of those floats.
 __global__ void __launch_bounds__(256) sigmoid_monotone_kernel(unsigned long long* bad) {
   constexpr unsigned kPer = 256, kEnd = 0x7F800000u;  // +inf
   const unsigned b0 = (blockIdx.x * 256u + threadIdx.x) * kPer;
   if (b0 >= kEnd) return;
   unsigned cnt = 0;
-  float pp = ycx_sigmoid(__uint_as_float(b0)), pn = ycx_sigmoid(__uint_as_float(b0 | 0x80000000u));
+  const float x0 = __uint_as_float(b0), y0 = __uint_as_float(b0 | 0x80000000u);
+  float pp = ycx_sigmoid(x0), pn = ycx_sigmoid(y0);
+  cnt += sigmoid_gap_bad(x0, pp) + sigmoid_gap_bad(y0, pn);
   for (unsigned i = 1; i <= kPer && b0 + i <= kEnd; ++i) {
     const unsigned b = b0 + i;
-    const float sp = ycx_sigmoid(__uint_as_float(b)), sn = ycx_sigmoid(__uint_as_float(b | 0x80000000u));
+    const float x = __uint_as_float(b), y = __uint_as_float(b | 0x80000000u);
+    const float sp = ycx_sigmoid(x), sn = ycx_sigmoid(y);
     cnt += (sp < pp ? 1u : 0u) + (sn > pn ? 1u : 0u);  // +x rising, -x falling with b
+    cnt += sigmoid_gap_bad(x, sp) + sigmoid_gap_bad(y, sn);
     pp = sp;
     pn = sn;
   }
