@@ -79,7 +79,10 @@ def test_tile_picker():
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 16  # ... which stores no residual
     d.res_c_stride = 0
     d.cout_pad, d.h, d.w, d.ho, d.wo = 512, 40, 40, 40, 40
+    assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 22  # >= 4 pixel tiles per persistent block (r06)
+    d.h = d.w = d.ho = d.wo = 20
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 16  # too few tiles per persistent block
+    d.h = d.w = d.ho = d.wo = 40
     d.kh, d.kw, d.pad = 3, 3, 1
     assert _lib.lib.ycx_conv_pick_tile(ctypes.byref(d)) == 48  # 40-wide 3x3, 1280 band workgroups
     d.cout_pad = 256

@@ -3710,7 +3710,10 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
         (d->cin == 128 || d->cin == 256 || d->cin == 512) &&
         (d->cout_pad == 64 || d->cout_pad == 128 || d->cout_pad % 256 == 0)) {
       const long long pt = d->cout_pad >= 256 ? 64 : 128, groups = d->cout_pad >= 256 ? d->cout_pad / 256 : 1;
-      if (M >= 8 * pt * (256 / groups)) return 36;
+#ifndef YCX_WRES_F8_MIN_TILES  // pixel tiles per persistent block (r06: 8 -> 4, as the bf16 tile 22)
+#define YCX_WRES_F8_MIN_TILES 4
+#endif
+      if (M >= YCX_WRES_F8_MIN_TILES * pt * (256 / groups)) return 36;
     }
     // 3x3 / s1 64 -> 64 'same' convs on 16-aligned maps with >= 2 tiles per block: weights in LDS (tile 37)
     if (allow_wres && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->h == d->ho &&
@@ -3741,7 +3744,10 @@ static int32_t pick_tile(const ycx_conv_desc* d, bool allow_wres) {  // allow_wr
       d->out_layout == YCX_OUT_NHWC && d->cin <= 512 && (d->cin & (d->cin - 1)) == 0 &&
       (d->cout_pad == 64 || d->cout_pad == 128 || d->cout_pad % 256 == 0)) {
     const long long pt = d->cout_pad >= 256 ? 64 : 128, groups = d->cout_pad >= 256 ? d->cout_pad / 256 : 1;
-    if (M >= 8 * pt * (256 / groups)) return 22;
+#ifndef YCX_WRES_MIN_TILES  // pixel tiles per persistent block (r06: 8 -> 4, the 40^2 512->512 and 80^2
+#define YCX_WRES_MIN_TILES 4  // 512->128 1x1s 50 -> 45-46 and 68 -> 66 us; 2 or 1 take slower 40^2 / 20^2 ones)
+#endif
+    if (M >= YCX_WRES_MIN_TILES * pt * (256 / groups)) return 22;
   }
   // 3x3 stride-1 'same' convs on 16-aligned maps: LDS halo tiles (tests/probes/conv_bench.py:
   // +14-18 % over the im2col tiles at 80^2 with >= 128 output channels, +18 % at 320^2 x 64)
