@@ -103,6 +103,11 @@ def parse(argv=None):
                     help="the north_star-conforming fp16 plan (1e-3 on box / confidence tensors) timed in the same "
                          "run after the headline leg, same mode (default: min(--steps, 30) when --precision is "
                          "bf16; 0: skip); reported as value_fp16 / ms_per_step_fp16 / roofline_fp16")
+    ap.add_argument("--pipelined-steps", type=int, default=None,
+                    help="the low-latency point of the same workload and precision timed in the same run: mode "
+                         "pipelined (two slots, forward and post on two streams) instead of the concurrent "
+                         "throughput mode (default: min(--steps, 30) in concurrent mode; 0: skip); reported as "
+                         "value_pipelined / ms_per_step_pipelined / p50_ms_pipelined")
     ap.add_argument("--round", default=None,
                     help="profiles/<round>/traffic.json for roofline.traffic (default: the newest round that has one)")
     ap.add_argument("--dry-run", action="store_true",
@@ -635,15 +640,17 @@ def timed_leg(args, det, mode, dist_on, gather, lat_ev, steps=None, latency_step
     return elapsed, lat, lat1, kc
 
 
-def precision_leg(args, dev, rank, world, dist_on, gather, mode, precision, steps):
-    """A second plan of the same workload in another precision, timed exactly as the
-    headline leg (warm-up, ``steps`` timed steps between barriers, max over ranks) in the
+def precision_leg(args, dev, rank, world, dist_on, gather, mode, precision, steps, sfx=None, with_roofline=True):
+    """A second plan of the same workload in another precision (or mode), timed exactly as
+    the headline leg (warm-up, ``steps`` timed steps between barriers, max over ranks) in the
     same run: the fp16 plan is the one that holds north_star's 1e-3 on box / confidence
-    tensors (detect.py:227-231 compares the reference's fp32 outputs). Returns the
-    ``*_<precision>`` keys of the JSON line."""
+    tensors (detect.py:227-231 compares the reference's fp32 outputs); the pipelined mode is
+    the low-latency point (BASELINE's p50 end-to-end latency). Returns the ``*<sfx>`` keys
+    of the JSON line (default suffix: ``_<precision>``)."""
     import copy
     a = copy.copy(args)
     a.precision = precision
+    a.mode = mode
     pipeline = False if mode == "serial" else mode
     _, det, _, _, _ = setup(a, dev, rank, pipeline=pipeline)
     lat_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
@@ -654,11 +661,12 @@ def precision_leg(args, dev, rank, world, dist_on, gather, mode, precision, step
     elapsed = float(t.item())
     value = world * args.batch * steps / elapsed
     det1 = det.slots[0] if pipeline else det
-    rl = roofline(det1, args.roofline_steps, precision) if rank == 0 else None
+    rl = roofline(det1, args.roofline_steps, precision) if rank == 0 and with_roofline else None
     det.close()
-    sfx = "_" + precision
+    sfx = sfx or "_" + precision
     out = {"value" + sfx: round(value, 2), "ms_per_step" + sfx: round(elapsed / steps * 1e3, 4),
-           "steps" + sfx: steps, "p50_ms" + sfx: round(statistics.median(lat), 4)}
+           "steps" + sfx: steps, "p50_ms" + sfx: round(statistics.median(lat), 4),
+           "p90_ms" + sfx: round(sorted(lat)[int(0.9 * (len(lat) - 1))], 4)}
     if rl is not None:
         peak = PEAK[precision]
         out["roofline" + sfx] = {"bound": "mfma", "kernel": rl['kernel'], "achieved": round(rl['achieved'], 2),
@@ -728,11 +736,18 @@ def main(argv=None):
     # the fp16 (north_star 1e-3) leg: at most 30 timed steps by default, so a long headline run
     # does not double the bench's wall time
     n16 = args.fp16_steps if args.fp16_steps is not None else (min(args.steps, 30) if args.precision == "bf16" else 0)
-    fp16 = None
-    if n16 > 0 and args.precision != "fp16" and not args.diag_forward_only:
-        det.close()  # the headline plan's HBM back before the second plan is built
+    npl = args.pipelined_steps if args.pipelined_steps is not None else (min(args.steps, 30) if mode == "concurrent"
+                                                                          else 0)
+    fp16 = pipelined = None
+    legs = not args.diag_forward_only and ((n16 > 0 and args.precision != "fp16") or (npl > 0 and mode == "concurrent"))
+    if legs:
+        det.close()  # the headline plan's HBM back before another plan is built
         del det, det1, model
+    if n16 > 0 and args.precision != "fp16" and not args.diag_forward_only:
         fp16 = precision_leg(args, dev, rank, world, dist_on, gather, mode, "fp16", n16)
+    if npl > 0 and mode == "concurrent" and not args.diag_forward_only:
+        pipelined = precision_leg(args, dev, rank, world, dist_on, gather, "pipelined", args.precision, npl,
+                                  sfx="_pipelined", with_roofline=False)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, sd, cfg)
@@ -777,6 +792,7 @@ def main(argv=None):
             "rccl_world_size": dist.get_world_size() if dist_on else 1,
             **(img_in or {}),
             **(fp16 or {}),
+            **(pipelined or {}),
             "detections_last_step": detections_last_step,
         }
         print(json.dumps(out), flush=True)

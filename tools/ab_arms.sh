@@ -7,7 +7,7 @@ R=${1:-r06}; shift
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$ROOT/gpurun_out/$R/arms
 mkdir -p "$O"
-FAST="--cpu-seconds 0 --fp16-steps 0 --image-in-steps 0 --latency-steps 0"
+FAST="--cpu-seconds 0 --fp16-steps 0 --pipelined-steps 0 --image-in-steps 0 --latency-steps 0"
 for r in $(seq 1 "${ROUNDS:-2}"); do
   for arm in "$@"; do
     name=${arm%%:*}

@@ -2,7 +2,7 @@
 # Same-box A/B of the concurrent bench (development tool), with the kernels-in-flight split of
 # each arm: A = yolo-continuous_amd/ycx/libycx_A.so (or A_ENV="VAR=value" on the in-tree library),
 # B = the in-tree library. Run through gpurun:  bash tools/ab_trace.sh r06 [bench args]
-# 1. the bench, A B A B (--cpu-seconds 0 --fp16-steps 0 --image-in-steps 0), per-op tables of both arms
+# 1. the bench, A B A B (--cpu-seconds 0 --fp16-steps 0 --pipelined-steps 0 --image-in-steps 0), per-op tables of both arms
 # 2. per arm (unless NO_TRACE=1): rocprofv3 --kernel-trace of the bench's timed loop -> tools/trace_busy.py
 R=${1:-r06}; shift
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -17,7 +17,7 @@ arm() {  # arm A|B: the environment of that arm
     [ -n "$A_ENV" ] && unset "${A_ENV%%=*}"
   fi
 }
-FAST="--cpu-seconds 0 --fp16-steps 0 --image-in-steps 0"
+FAST="--cpu-seconds 0 --fp16-steps 0 --pipelined-steps 0 --image-in-steps 0"
 for v in A B A B; do
   arm $v
   YCX_BENCH_KERNELS=$O/ops_$v.json timeout -k 10 300 python "$ROOT/bench.py" $FAST "$@" > "$O/bench_$v.log" 2>&1 || { tail -5 "$O/bench_$v.log"; exit 1; }

@@ -1,7 +1,7 @@
 cd /tmp && export TMPDIR=/tmp
 O=$GRAFT_REPO_ROOT/gpurun_out/r06cp
 mkdir -p $O
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/p -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --cpu-seconds 0 --fp16-steps 0 --image-in-steps 0 --latency-steps 0 --roofline-steps 1 --steps 50 > $O/b.log 2>&1 || { tail -5 $O/b.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/p -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --cpu-seconds 0 --fp16-steps 0 --pipelined-steps 0 --image-in-steps 0 --latency-steps 0 --roofline-steps 1 --steps 50 > $O/b.log 2>&1 || { tail -5 $O/b.log; exit 1; }
 f=$(find $O/p -name '*kernel_stats.csv' | head -n 1); cp $f $O/stats.csv
 t=$(find $O/p -name '*kernel_trace.csv' | head -n 1); python3 - "$t" <<'P'
 import csv,sys,collections

@@ -19,7 +19,7 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 YCX_BENCH_KERNELS=$OUT/ops.json timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run \
-  --output-format csv -- python3 "$ROOT/bench.py" --fp16-steps 0 --cpu-seconds 0 > "$OUT/bench_under_rocprof.log" 2>&1
+  --output-format csv -- python3 "$ROOT/bench.py" --fp16-steps 0 --pipelined-steps 0 --cpu-seconds 0 > "$OUT/bench_under_rocprof.log" 2>&1
 TRACE=$(find "$OUT/trace" -name '*kernel_trace.csv' | head -n 1)
 NOPS=$(python3 -c "import json; print(len(json.load(open('$OUT/ops.json'))['ops']))")
 python3 "$ROOT/tools/trace_leg_stats.py" "$TRACE" "$NOPS" 3 "$OUT/kernel_stats_roofline_leg.csv" > "$OUT/trace_legs.txt"

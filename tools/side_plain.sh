@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 cd "$ROOT"
 run() {  # name, bench args...
   local name=$1; shift
-  timeout -k 10 300 python3 bench.py --cpu-seconds 0 --fp16-steps 0 "$@" > "$OUT/plain_$name.log" 2>&1
+  timeout -k 10 300 python3 bench.py --cpu-seconds 0 --fp16-steps 0 --pipelined-steps 0 "$@" > "$OUT/plain_$name.log" 2>&1
   grep '^{"metric' "$OUT/plain_$name.log" | tail -n 1 > "$OUT/plain_$name.json"
   cut -c1-160 "$OUT/plain_$name.json"
 }

@@ -3,7 +3,7 @@
     python tools/trace_busy.py gpurun_out/r05/busy/.../run_kernel_trace.csv [skip_frac]
 
 Takes the kernels of the timed loop of `bench.py --latency-steps 0 --image-in-steps 0
---cpu-seconds 0 --fp16-steps 0 --roofline-steps 1`: the longest run of dispatches with no
+--cpu-seconds 0 --fp16-steps 0 --pipelined-steps 0 --roofline-steps 1`: the longest run of dispatches with no
 kernel on the default stream (the slot streams of the concurrent detector only; set-up
 copies, graph capture and the serial roofline leg run on the default stream), less its
 first and last `skip_frac` so the warm-up / drain edges do not count, and prints: the fraction of wall time at least one

@@ -208,12 +208,21 @@ def check(status: int, what: str = "") -> None:
         raise YcxError(status, what)
 
 
-def dedicated_stream(device, priority: int = 0):
+def dedicated_stream(device, priority: int = 0, slot: int | None = None):
     """A non-blocking HIP stream of our own (hipStreamCreateWithPriority), wrapped
     as a torch ExternalStream: unlike torch.cuda.Stream() it is not one of the
     pool streams that every other component (the RCCL communicator included)
-    is handed round-robin, so no other work can share it. Never destroyed."""
+    is handed round-robin, so no other work can share it. Never destroyed, so
+    ``slot`` streams are kept per (device, priority, slot) and handed out again:
+    detectors built one after another (bench.py's legs) reuse the same few
+    streams instead of piling up more streams than the GPU has hardware queues
+    (GPU_MAX_HW_QUEUES, 4), which slowed every later leg (r06: the pipelined leg
+    after the fp16 leg ran 8.7 instead of 5.2 ms per step)."""
     import torch
+    dev = torch.device(device)
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), priority, slot)
+    if slot is not None and key in _SLOT_STREAMS:
+        return torch.cuda.ExternalStream(_SLOT_STREAMS[key], device=device)
     hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already loaded (same soname)
     s = ctypes.c_void_p()
     with torch.cuda.device(device):
@@ -221,9 +230,12 @@ def dedicated_stream(device, priority: int = 0):
     if rc != 0:
         raise RuntimeError(f"ycx: hipStreamCreateWithPriority failed ({rc})")
     _STREAMS.append(s.value)
+    if slot is not None:
+        _SLOT_STREAMS[key] = s.value
     return torch.cuda.ExternalStream(s.value, device=device)
 
 
+_SLOT_STREAMS = {}
 _STREAMS = []
 
 

@@ -478,7 +478,7 @@ class ConcurrentDetector:
         # slot stream that shares its hardware queue with the communicator's
         # serialises every batch behind the previous batch's all-gather
         # (tests/probes/dist_probe.py: 7.8 vs 6.0 ms per step)
-        self.streams = [L.dedicated_stream(self.device, 0) for _ in self.slots]
+        self.streams = [L.dedicated_stream(self.device, 0, slot=i) for i in range(len(self.slots))]
         self.done = [torch.cuda.Event() for _ in self.slots]
         self.i = 0
 
